@@ -1,0 +1,151 @@
+#!/usr/bin/env python
+"""Headline benchmark: DDP training throughput at seq_len=2048, bf16, on 1..8 MI355X.
+
+Measures the reference's headline metric (tokens/sec at seq 2048 bf16, BASELINE.json) on the
+Llama-2-7B-shape transformer of BASELINE.json config 3 (dim 4096, 32 layers, 32 heads, SwiGLU
+11008, vocab 32000), random-init weights, synthetic token data. Each timed step is a full
+training step: forward, backward with bucketed RCCL gradient all-reduce (N>1), fused AdamW
+update and LR-scheduler step -- nothing is skipped.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it is launched by
+``torch.distributed.run`` (one rank per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* from env).
+Rank 0 prints ONE JSON line; ``value`` is the whole-job aggregate tokens/s (max time over ranks).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", default="llama2-7b")
+    ap.add_argument("--seq-len", type=int, default=2048)
+    ap.add_argument("--batch-per-gpu", type=int, default=4)
+    ap.add_argument("--bucket-mb", type=float, default=256.0)
+    ap.add_argument("--lr", type=float, default=1e-5)
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--profile-steps", type=int, default=0, help="emit roctx ranges for this many steps")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from pyrecover_amd.config import get_preset
+    from pyrecover_amd.models.llama import Transformer
+    from pyrecover_amd.optim.adamw import FlatAdamW
+    from pyrecover_amd.optim.lr import build_lr_scheduler
+    from pyrecover_amd.parallel import dist as D
+    from pyrecover_amd.parallel.ddp import GradReducer, broadcast_flat
+    from pyrecover_amd.utils.flops import num_flop_per_token
+
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env > 1:
+        lrank, world = D.maybe_init_distributed(True)
+    else:
+        lrank, world = 0, 1
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    dev = torch.device("cuda", lrank)
+    torch.cuda.set_device(dev)
+    rank = D.get_rank()
+
+    cfg = get_preset(args.model, seq_len=args.seq_len)
+    torch.manual_seed(args.seed)
+    with torch.device(dev):
+        prev = torch.get_default_dtype()
+        torch.set_default_dtype(torch.bfloat16)
+        model = Transformer(cfg)
+        torch.set_default_dtype(prev)
+    flat = model.flatten_()
+    reducer = None
+    if world > 1:
+        broadcast_flat(flat)
+        reducer = GradReducer(flat, bucket_cap_mb=args.bucket_mb)
+    opt = FlatAdamW(flat, lr=args.lr, fused=True, grad_scale=1.0 / world)
+    sched = build_lr_scheduler(opt, 10)
+
+    B, S = args.batch_per_gpu, args.seq_len
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(args.seed * 1000 + rank)
+
+    def batch():
+        t = torch.randint(0, cfg.vocab_size, (B, S + 1), device=dev, generator=gen)
+        return t[:, :-1], t[:, 1:]
+
+    def step():
+        x, y = batch()
+        opt.zero_grad()
+        loss = model(x, labels=y)
+        loss.backward()
+        if reducer is not None:
+            reducer.finish()
+        opt.step()
+        sched.step()
+        return loss
+
+    for _ in range(args.warmup):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        if args.profile_steps and i < args.profile_steps:
+            torch.cuda.nvtx.range_push(f"step{i}")
+        loss = step()
+        if args.profile_steps and i < args.profile_steps:
+            torch.cuda.nvtx.range_pop()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    dt_t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    if world > 1:
+        torch.distributed.all_reduce(dt_t, op=torch.distributed.ReduceOp.MAX)
+    dt = float(dt_t.item())
+    final_loss = float(loss.item())
+    tokens = B * S * world * args.steps
+    tps = tokens / dt
+    n_params = model.num_params()
+    fpt = num_flop_per_token(model.num_params(exclude_embedding=True), cfg)
+    if rank == 0:
+        out = {
+            "metric": "tokens/sec at seq=2048 bf16 (job aggregate over all GPUs; per-GPU in tokens_per_sec_per_gpu)",
+            "value": round(tps, 2),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000 * dt / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (uniform random token ids), random-init weights",
+            "config": {"model": f"{args.model}-shape ({n_params / 1e9:.2f}B params)", "global_batch": B * world,
+                       "seq_len": S, "parallelism": f"dp{world}", "batch_per_gpu": B,
+                       "bucket_mb": args.bucket_mb if world > 1 else None, "optimizer": "AdamW (flat fused HIP)"},
+            "tokens_per_sec_per_gpu": round(tps / world, 2),
+            "model_tflops_per_gpu": round(fpt * tps / world / 1e12, 2),
+            "mfu_pct_vs_2.5PF": round(100 * fpt * tps / world / 2.5e15, 2),
+            "final_loss": round(final_loss, 4),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

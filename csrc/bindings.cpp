@@ -1,0 +1,309 @@
+// Torch <-> HIP kernel adapter for pyrecover_amd._C.
+//
+// Every op validates shapes/strides/dtypes on the host BEFORE launching (a mis-shaped launch
+// of a hand-written kernel could fault the GPU), then calls the raw launcher on the current
+// HIP stream of the tensor's device.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+
+#include "kernels/launchers.h"
+
+namespace {
+
+int dt(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return 0;
+    case at::kBFloat16: return 1;
+    case at::kHalf: return 2;
+    default: TORCH_CHECK(false, "pyrecover_amd: unsupported dtype ", t.scalar_type());
+  }
+}
+
+hipStream_t stream_of(const at::Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+void check(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, "pyrecover_amd: ", what, " failed: ", hipGetErrorString(e));
+}
+
+void check_dev(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "pyrecover_amd: ", name, " must be a GPU tensor");
+}
+
+void check_row_major(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1, "pyrecover_amd: ", name, " must be 2-D with unit inner stride");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "pyrecover_amd: ", name, " must be 16-B aligned");
+}
+
+// ---------------------------------------------------------------------------------------
+std::vector<at::Tensor> rmsnorm_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& delta, const at::Tensor& w,
+                                    double eps) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.is_contiguous() && w.is_contiguous(), "rmsnorm_fwd: x and w must be contiguous");
+  const int64_t D = x.size(-1);
+  const int64_t rows = x.numel() / D;
+  TORCH_CHECK(w.numel() == D && w.scalar_type() == x.scalar_type(), "rmsnorm_fwd: weight mismatch");
+  TORCH_CHECK(D % 8 == 0 && D <= 8192, "rmsnorm_fwd: D must be a multiple of 8 and <= 8192");
+  const c10::hip::HIPGuard guard(x.device());
+  at::Tensor y = at::empty_like(x);
+  at::Tensor rstd = at::empty({rows}, x.options().dtype(at::kFloat));
+  at::Tensor h;
+  const void* dptr = nullptr;
+  if (delta.has_value()) {
+    TORCH_CHECK(delta->sizes() == x.sizes() && delta->is_contiguous() && delta->scalar_type() == x.scalar_type(),
+                "rmsnorm_fwd: delta mismatch");
+    h = at::empty_like(x);
+    dptr = delta->data_ptr();
+  }
+  check(pra_rmsnorm_fwd(dt(x), x.data_ptr(), dptr, w.data_ptr(), h.defined() ? h.data_ptr() : nullptr,
+                        y.data_ptr(), rstd.data_ptr<float>(), (int)rows, (int)D, (float)eps, stream_of(x)),
+        "rmsnorm_fwd");
+  return {h.defined() ? h : x, y, rstd};
+}
+
+at::Tensor rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at::Tensor& w, const at::Tensor& rstd,
+                       const c10::optional<at::Tensor>& dres, at::Tensor dw, bool accumulate) {
+  check_dev(dy, "dy");
+  TORCH_CHECK(dy.is_contiguous() && h.is_contiguous() && dy.sizes() == h.sizes(), "rmsnorm_bwd: dy/h mismatch");
+  const int64_t D = h.size(-1);
+  const int64_t rows = h.numel() / D;
+  TORCH_CHECK(w.numel() == D && dw.numel() == D && dw.is_contiguous() && rstd.numel() == rows,
+              "rmsnorm_bwd: shape mismatch");
+  TORCH_CHECK(dw.scalar_type() == h.scalar_type() && dy.scalar_type() == h.scalar_type(), "rmsnorm_bwd: dtype");
+  const c10::hip::HIPGuard guard(h.device());
+  at::Tensor dx = at::empty_like(h);
+  const void* dr = nullptr;
+  if (dres.has_value()) {
+    TORCH_CHECK(dres->sizes() == h.sizes() && dres->is_contiguous() && dres->scalar_type() == h.scalar_type(),
+                "rmsnorm_bwd: dres mismatch");
+    dr = dres->data_ptr();
+  }
+  const int wsr = pra_rmsnorm_bwd_ws_rows((int)rows);
+  at::Tensor ws = at::empty({wsr, D}, h.options().dtype(at::kFloat));
+  check(pra_rmsnorm_bwd(dt(h), dy.data_ptr(), h.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(), dr, dx.data_ptr(),
+                        dw.data_ptr(), ws.data_ptr<float>(), (int)rows, (int)D, accumulate ? 1 : 0, stream_of(h)),
+        "rmsnorm_bwd");
+  return dx;
+}
+
+// In-place RoPE on the first `ncols` columns of each row of a 2-D [tokens, ld] buffer.
+void rope_(at::Tensor x2d, int64_t ncols, const at::Tensor& tab, int64_t head_dim, int64_t seq_len,
+           int64_t pos_offset, bool inverse) {
+  check_dev(x2d, "x");
+  check_row_major(x2d, "rope x");
+  TORCH_CHECK(tab.scalar_type() == at::kFloat && tab.is_contiguous(), "rope: table must be contiguous fp32");
+  TORCH_CHECK(tab.numel() >= (seq_len + pos_offset) * head_dim, "rope: table too small");
+  TORCH_CHECK(ncols <= x2d.size(1) && ncols % head_dim == 0 && head_dim % 8 == 0, "rope: bad ncols/head_dim");
+  TORCH_CHECK(x2d.size(0) % seq_len == 0, "rope: tokens must be a multiple of seq_len");
+  const c10::hip::HIPGuard guard(x2d.device());
+  check(pra_rope(dt(x2d), x2d.data_ptr(), tab.data_ptr(), x2d.size(0), (int)x2d.stride(0), (int)ncols, (int)head_dim,
+                 (int)seq_len, (int)pos_offset, inverse ? 1 : 0, stream_of(x2d)),
+        "rope");
+}
+
+// gu: [T, 2F] (gate | up) -> y [T, F]
+at::Tensor swiglu_fwd(const at::Tensor& gu) {
+  check_dev(gu, "gu");
+  check_row_major(gu, "gu");
+  TORCH_CHECK(gu.size(1) % 16 == 0, "swiglu: 2F must be a multiple of 16");
+  const int64_t F = gu.size(1) / 2;
+  const c10::hip::HIPGuard guard(gu.device());
+  at::Tensor y = at::empty({gu.size(0), F}, gu.options());
+  const char* base = (const char*)gu.data_ptr();
+  check(pra_swiglu_fwd(dt(gu), base, base + F * gu.element_size(), y.data_ptr(), gu.size(0), (int)F,
+                       (int)gu.stride(0), (int)gu.stride(0), (int)F, stream_of(gu)),
+        "swiglu_fwd");
+  return y;
+}
+
+// dgu may alias gu (in-place backward).
+at::Tensor swiglu_bwd(const at::Tensor& dy, const at::Tensor& gu, c10::optional<at::Tensor> out) {
+  check_dev(gu, "gu");
+  check_row_major(gu, "gu");
+  check_row_major(dy, "dy");
+  const int64_t F = gu.size(1) / 2;
+  TORCH_CHECK(dy.size(0) == gu.size(0) && dy.size(1) == F && dy.scalar_type() == gu.scalar_type(), "swiglu_bwd: dy");
+  const c10::hip::HIPGuard guard(gu.device());
+  at::Tensor dgu = out.has_value() ? *out : at::empty_like(gu);
+  TORCH_CHECK(dgu.sizes() == gu.sizes() && dgu.strides() == gu.strides(), "swiglu_bwd: out layout");
+  const char* g = (const char*)gu.data_ptr();
+  char* o = (char*)dgu.data_ptr();
+  const int64_t es = gu.element_size();
+  check(pra_swiglu_bwd(dt(gu), dy.data_ptr(), g, g + F * es, o, o + F * es, gu.size(0), (int)F, (int)gu.stride(0),
+                       (int)gu.stride(0), (int)dy.stride(0), stream_of(gu)),
+        "swiglu_bwd");
+  return dgu;
+}
+
+at::Tensor embedding_fwd(const at::Tensor& ids, const at::Tensor& W) {
+  check_dev(W, "W");
+  TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous() && ids.device() == W.device(),
+              "embedding: ids must be contiguous int64 on the weight's device");
+  TORCH_CHECK(W.dim() == 2 && W.is_contiguous() && W.size(1) % 8 == 0, "embedding: bad weight");
+  const c10::hip::HIPGuard guard(W.device());
+  auto sizes = ids.sizes().vec();
+  sizes.push_back(W.size(1));
+  at::Tensor out = at::empty(sizes, W.options());
+  check(pra_embedding_fwd(dt(W), ids.data_ptr<int64_t>(), W.data_ptr(), out.data_ptr(), ids.numel(), (int)W.size(1),
+                          W.size(0), stream_of(W)),
+        "embedding_fwd");
+  return out;
+}
+
+// Deterministic dense embedding gradient into dW (overwrites unless accumulate).
+void embedding_bwd(const at::Tensor& ids, const at::Tensor& dout, at::Tensor dW, bool accumulate) {
+  check_dev(dW, "dW");
+  TORCH_CHECK(dW.is_contiguous() && dout.is_contiguous() && dout.size(-1) == dW.size(1), "embedding_bwd: shapes");
+  TORCH_CHECK(dout.numel() / dW.size(1) == ids.numel(), "embedding_bwd: ids/dout mismatch");
+  const c10::hip::HIPGuard guard(dW.device());
+  auto flat = ids.reshape({-1});
+  auto sorted = at::sort(flat, /*stable=*/true, /*dim=*/0, /*descending=*/false);
+  at::Tensor sids = std::get<0>(sorted).contiguous();
+  at::Tensor perm = std::get<1>(sorted).contiguous();
+  if (!accumulate) dW.zero_();
+  check(pra_embedding_bwd(dt(dW), sids.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), dout.data_ptr(), dW.data_ptr(),
+                          flat.numel(), (int)dW.size(1), dW.size(0), accumulate ? 1 : 0, stream_of(dW)),
+        "embedding_bwd");
+}
+
+// logits [T, V] (row stride ld), labels [T] -> (lse [T], loss_row [T], stats [2] = {mean loss, n_valid})
+std::vector<at::Tensor> xent_fwd(const at::Tensor& logits, const at::Tensor& labels, int64_t ignore_index) {
+  check_dev(logits, "logits");
+  check_row_major(logits, "logits");
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_contiguous() && labels.numel() == logits.size(0),
+              "xent: labels must be contiguous int64 [T]");
+  const c10::hip::HIPGuard guard(logits.device());
+  const int64_t T = logits.size(0);
+  auto fo = logits.options().dtype(at::kFloat);
+  at::Tensor lse = at::empty({T}, fo), loss_row = at::empty({T}, fo), stats = at::empty({2}, fo);
+  check(pra_xent_fwd(dt(logits), logits.data_ptr(), labels.data_ptr<int64_t>(), lse.data_ptr<float>(),
+                     loss_row.data_ptr<float>(), stats.data_ptr<float>(), T, logits.size(1), logits.stride(0),
+                     ignore_index, stream_of(logits)),
+        "xent_fwd");
+  return {lse, loss_row, stats};
+}
+
+void xent_bwd_(at::Tensor logits, const at::Tensor& labels, const at::Tensor& lse, const at::Tensor& stats,
+               const at::Tensor& grad_out, int64_t ignore_index) {
+  check_dev(logits, "logits");
+  check_row_major(logits, "logits");
+  TORCH_CHECK(grad_out.scalar_type() == at::kFloat && grad_out.numel() == 1 && grad_out.is_cuda(),
+              "xent_bwd: grad_out must be a 1-element fp32 GPU tensor");
+  const c10::hip::HIPGuard guard(logits.device());
+  check(pra_xent_bwd(dt(logits), logits.data_ptr(), labels.data_ptr<int64_t>(), lse.data_ptr<float>(),
+                     stats.data_ptr<float>(), grad_out.data_ptr<float>(), logits.size(0), logits.size(1),
+                     logits.stride(0), ignore_index, stream_of(logits)),
+        "xent_bwd");
+}
+
+void adamw_flat_(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, double lr, double b1, double b2,
+                 double eps, double wd, double bc1, double bc2_sqrt, double gscale,
+                 const c10::optional<at::Tensor>& gscale_dev) {
+  check_dev(p, "p");
+  TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous(), "adamw: contiguous");
+  TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(), "adamw: sizes");
+  TORCH_CHECK(g.scalar_type() == p.scalar_type() && m.scalar_type() == v.scalar_type(), "adamw: dtypes");
+  const c10::hip::HIPGuard guard(p.device());
+  const float* gsd = nullptr;
+  if (gscale_dev.has_value()) {
+    TORCH_CHECK(gscale_dev->scalar_type() == at::kFloat && gscale_dev->is_cuda(), "adamw: gscale_dev fp32 GPU");
+    gsd = gscale_dev->data_ptr<float>();
+  }
+  check(pra_adamw_flat(dt(p), dt(m), p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), (float)lr,
+                       (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1, (float)bc2_sqrt, (float)gscale, gsd,
+                       stream_of(p)),
+        "adamw_flat");
+}
+
+// returns fp32 [2] = {norm, clip_coef}
+at::Tensor grad_norm(const at::Tensor& x, double max_norm, double pre_scale) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.is_contiguous(), "grad_norm: contiguous");
+  const c10::hip::HIPGuard guard(x.device());
+  auto fo = x.options().dtype(at::kFloat);
+  at::Tensor ws = at::empty({pra_sumsq_partials()}, fo), out = at::empty({2}, fo);
+  check(pra_grad_norm(dt(x), x.data_ptr(), x.numel(), ws.data_ptr<float>(), out.data_ptr<float>(), (float)max_norm,
+                      (float)pre_scale, stream_of(x)),
+        "grad_norm");
+  return out;
+}
+
+// q/k/v/o views [B, S, H, D] with stride(3)==1, stride(2)==D, stride(0)==S*stride(1).
+void check_bshd(const at::Tensor& t, const char* name, int64_t B, int64_t S, int64_t H, int64_t D) {
+  TORCH_CHECK(t.dim() == 4 && t.size(0) == B && t.size(1) == S && t.size(2) == H && t.size(3) == D,
+              "attention: ", name, " must be [B, S, H, D] = [", B, ", ", S, ", ", H, ", ", D, "], got ", t.sizes());
+  TORCH_CHECK(t.stride(3) == 1 && t.stride(2) == D && t.stride(0) == S * t.stride(1),
+              "attention: ", name, " must have token-major layout with contiguous heads, strides ", t.strides());
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, "attention: ", name, " must be bf16");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "attention: ", name, " must be 16-B aligned");
+}
+
+std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale,
+                                 bool causal) {
+  check_dev(q, "q");
+  const int64_t B = q.size(0), S = q.size(1), Hq = q.size(2), D = q.size(3), Hkv = k.size(2);
+  check_bshd(q, "q", B, S, Hq, D);
+  check_bshd(k, "k", B, S, Hkv, D);
+  check_bshd(v, "v", B, S, Hkv, D);
+  TORCH_CHECK(S % 64 == 0, "attention: seq_len must be a multiple of 64");
+  TORCH_CHECK(D == 64 || D == 128, "attention: head_dim must be 64 or 128");
+  TORCH_CHECK(Hq % Hkv == 0, "attention: n_heads must be a multiple of n_kv_heads");
+  const c10::hip::HIPGuard guard(q.device());
+  at::Tensor o = at::empty({B, S, Hq, D}, q.options());
+  at::Tensor lse = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
+  check(pra_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), (int)B, (int)S,
+                     (int)Hq, (int)Hkv, (int)D, q.stride(1), k.stride(1), v.stride(1), o.stride(1), (float)scale,
+                     causal ? 1 : 0, stream_of(q)),
+        "attn_fwd");
+  return {o, lse};
+}
+
+// Writes dq/dk/dv into caller-provided [B,S,H,D] views (e.g. slices of a fused dQKV buffer).
+void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const at::Tensor& o,
+              const at::Tensor& dout, const at::Tensor& lse, at::Tensor dq, at::Tensor dk, at::Tensor dv, double scale,
+              bool causal) {
+  check_dev(q, "q");
+  const int64_t B = q.size(0), S = q.size(1), Hq = q.size(2), D = q.size(3), Hkv = k.size(2);
+  check_bshd(q, "q", B, S, Hq, D);
+  check_bshd(k, "k", B, S, Hkv, D);
+  check_bshd(v, "v", B, S, Hkv, D);
+  check_bshd(o, "o", B, S, Hq, D);
+  check_bshd(dout, "dout", B, S, Hq, D);
+  check_bshd(dq, "dq", B, S, Hq, D);
+  check_bshd(dk, "dk", B, S, Hkv, D);
+  check_bshd(dv, "dv", B, S, Hkv, D);
+  TORCH_CHECK(S % 128 == 0, "attention backward: seq_len must be a multiple of 128");
+  TORCH_CHECK(D == 64 || D == 128, "attention: head_dim must be 64 or 128");
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.numel() == B * Hq * S && lse.is_contiguous(), "attention: lse");
+  const c10::hip::HIPGuard guard(q.device());
+  at::Tensor delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
+  check(pra_attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
+                     delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), (int)B, (int)S, (int)Hq,
+                     (int)Hkv, (int)D, q.stride(1), k.stride(1), v.stride(1), o.stride(1), dout.stride(1), dq.stride(1),
+                     dk.stride(1), dv.stride(1), (float)scale, causal ? 1 : 0, stream_of(q)),
+        "attn_bwd");
+}
+
+}  // namespace
+
+void register_ckpt_engine(pybind11::module& m);  // csrc/runtime/ckpt_engine.cpp
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "pyrecover_amd native ops (HIP/gfx950 kernels + checkpoint engine)";
+  m.def("rmsnorm_fwd", &rmsnorm_fwd);
+  m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("rope_", &rope_);
+  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("embedding_fwd", &embedding_fwd);
+  m.def("embedding_bwd", &embedding_bwd);
+  m.def("xent_fwd", &xent_fwd);
+  m.def("xent_bwd_", &xent_bwd_);
+  m.def("adamw_flat_", &adamw_flat_);
+  m.def("grad_norm", &grad_norm);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
+  register_ckpt_engine(m);
+}

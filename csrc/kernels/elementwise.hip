@@ -1,0 +1,204 @@
+// Memory-bound elementwise kernels: RoPE (in place on the fused QKV activation), SwiGLU
+// forward/backward, embedding gather + deterministic embedding backward.
+//
+// All kernels move 8 elements (16 B for bf16) per lane and use grid-stride loops capped at
+// 256 CUs x 8 blocks, per the CDNA4 memory-bound recipe.
+#include "common.h"
+
+namespace pra {
+
+static inline int grid_for(size_t work_items, int block = 256) {
+  size_t g = (work_items + block - 1) / block;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+// ----------------------------------------------------------------------------------------
+// RoPE, interleaved-pair convention of the reference (model.py:101-127): the pair
+// (x[2i], x[2i+1]) is multiplied by cis(pos * freq_i) in fp32 and rounded back.
+// x points at the first rotated column of token 0; `ld` is the token row stride; the first
+// `ncols` columns of each row (q heads followed by k heads, head_dim D each) are rotated.
+// tab is float2[S][D/2] = (cos, sin). sign = -1 applies the inverse rotation (backward).
+template <typename T>
+__global__ __launch_bounds__(256) void rope_kernel(T* __restrict__ x, const float2* __restrict__ tab,
+                                                   long ntok, int ld, int ncols, int D, int S,
+                                                   int pos_offset, float sign) {
+  const int vpr = ncols / 8;  // 8-element vectors per row
+  const long total = ntok * vpr;
+  for (long idx = (long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
+    const long t = idx / vpr;
+    const int col = (int)(idx - t * vpr) * 8;
+    const int pos = (int)(t % S) + pos_offset;
+    const int pi = (col % D) / 2;  // first pair index
+    T* p = x + t * (long)ld + col;
+    float v[8];
+    load8<T>(p, v);
+    const float4* tp = reinterpret_cast<const float4*>(tab + (size_t)pos * (D / 2) + pi);
+    float4 cs01 = tp[0], cs23 = tp[1];
+    float c[4] = {cs01.x, cs01.z, cs23.x, cs23.z};
+    float s[4] = {cs01.y * sign, cs01.w * sign, cs23.y * sign, cs23.w * sign};
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float a = v[2 * k], b = v[2 * k + 1];
+      o[2 * k] = a * c[k] - b * s[k];
+      o[2 * k + 1] = a * s[k] + b * c[k];
+    }
+    store8<T>(p, o);
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// SwiGLU (reference model.py:268-269, `w2(silu(w1 x) * w3 x)`), with the reference's bf16
+// rounding points: a = round(silu(g)), y = round(a * u).
+__device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
+
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const T* __restrict__ g, const T* __restrict__ u,
+                                                         T* __restrict__ y, long ntok, int F, int ldg,
+                                                         int ldu, int ldy) {
+  const int vpr = F / 8;
+  const long total = ntok * vpr;
+  for (long idx = (long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
+    const long t = idx / vpr;
+    const int col = (int)(idx - t * vpr) * 8;
+    float gv[8], uv[8], o[8];
+    load8<T>(g + t * ldg + col, gv);
+    load8<T>(u + t * ldu + col, uv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = rnd<T>(silu_f(gv[j])) * uv[j];
+    store8<T>(y + t * ldy + col, o);
+  }
+}
+
+// dg = silu'(g) * round(dy * u), du = round(dy * round(silu(g)))
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_bwd_kernel(const T* __restrict__ dy, const T* g, const T* u,
+                                                         T* dg, T* du, long ntok, int F, int ldg, int ldu,
+                                                         int lddy) {
+  const int vpr = F / 8;
+  const long total = ntok * vpr;
+  for (long idx = (long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
+    const long t = idx / vpr;
+    const int col = (int)(idx - t * vpr) * 8;
+    float gv[8], uv[8], dv[8], og[8], ou[8];
+    load8<T>(g + t * ldg + col, gv);
+    load8<T>(u + t * ldu + col, uv);
+    load8<T>(dy + t * lddy + col, dv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float sg = 1.f / (1.f + __expf(-gv[j]));
+      const float a = rnd<T>(gv[j] * sg);
+      const float da = rnd<T>(dv[j] * uv[j]);
+      ou[j] = dv[j] * a;
+      og[j] = da * sg * (1.f + gv[j] * (1.f - sg));
+    }
+    store8<T>(dg + t * ldg + col, og);
+    store8<T>(du + t * ldu + col, ou);
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// Embedding gather: out[t] = W[ids[t]]; one wave per token.
+template <typename T>
+__global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restrict__ ids, const T* __restrict__ W,
+                                                        T* __restrict__ out, long ntok, int D, long V) {
+  const int lane = threadIdx.x & 63;
+  const long t = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= ntok) return;
+  long id = ids[t];
+  if (id < 0 || id >= V) id = 0;  // out-of-range ids are a caller bug; never read out of bounds
+  const T* src = W + id * (long)D;
+  T* dst = out + t * (long)D;
+  for (int c = lane * 8; c < D; c += 512) {
+    float v[8];
+    load8<T>(src + c, v);
+    store8<T>(dst + c, v);
+  }
+}
+
+// Deterministic embedding backward over ids sorted (stably) ascending: the wave that owns a
+// segment start sums the segment's dout rows in sorted (= original token) order.
+template <typename T>
+__global__ __launch_bounds__(256) void embed_bwd_kernel(const int64_t* __restrict__ sorted_ids,
+                                                        const int64_t* __restrict__ perm, const T* __restrict__ dout,
+                                                        T* __restrict__ dW, long ntok, int D, long V,
+                                                        int accumulate) {
+  const int lane = threadIdx.x & 63;
+  const long i = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= ntok) return;
+  const long v = sorted_ids[i];
+  if (i > 0 && sorted_ids[i - 1] == v) return;
+  if (v < 0 || v >= V) return;
+  long end = i + 1;
+  while (end < ntok && sorted_ids[end] == v) ++end;
+  for (int c = lane * 8; c < D; c += 512) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (accumulate) load8<T>(dW + v * (long)D + c, acc);
+    for (long j = i; j < end; ++j) {
+      float r[8];
+      load8<T>(dout + perm[j] * (long)D + c, r);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += r[k];
+    }
+    store8<T>(dW + v * (long)D + c, acc);
+  }
+}
+
+}  // namespace pra
+
+extern "C" {
+
+hipError_t pra_rope(int dtype, void* x, const void* tab, long ntok, int ld, int ncols, int D, int S,
+                    int pos_offset, int inverse, hipStream_t s) {
+  if (ncols % 8 || D % 8 || ld % 8) return hipErrorInvalidValue;
+  const int grid = pra::grid_for((size_t)ntok * (ncols / 8));
+  PRA_DISPATCH_FLOAT(dtype, T,
+                     hipLaunchKernelGGL((pra::rope_kernel<T>), dim3(grid), dim3(256), 0, s, (T*)x,
+                                        (const float2*)tab, ntok, ld, ncols, D, S, pos_offset,
+                                        inverse ? -1.f : 1.f));
+  return hipGetLastError();
+}
+
+hipError_t pra_swiglu_fwd(int dtype, const void* g, const void* u, void* y, long ntok, int F, int ldg,
+                          int ldu, int ldy, hipStream_t s) {
+  if (F % 8 || ldg % 8 || ldu % 8 || ldy % 8) return hipErrorInvalidValue;
+  const int grid = pra::grid_for((size_t)ntok * (F / 8));
+  PRA_DISPATCH_FLOAT(dtype, T,
+                     hipLaunchKernelGGL((pra::swiglu_fwd_kernel<T>), dim3(grid), dim3(256), 0, s, (const T*)g,
+                                        (const T*)u, (T*)y, ntok, F, ldg, ldu, ldy));
+  return hipGetLastError();
+}
+
+hipError_t pra_swiglu_bwd(int dtype, const void* dy, const void* g, const void* u, void* dg, void* du,
+                          long ntok, int F, int ldg, int ldu, int lddy, hipStream_t s) {
+  if (F % 8 || ldg % 8 || ldu % 8 || lddy % 8) return hipErrorInvalidValue;
+  const int grid = pra::grid_for((size_t)ntok * (F / 8));
+  PRA_DISPATCH_FLOAT(dtype, T,
+                     hipLaunchKernelGGL((pra::swiglu_bwd_kernel<T>), dim3(grid), dim3(256), 0, s, (const T*)dy,
+                                        (const T*)g, (const T*)u, (T*)dg, (T*)du, ntok, F, ldg, ldu, lddy));
+  return hipGetLastError();
+}
+
+hipError_t pra_embedding_fwd(int dtype, const int64_t* ids, const void* W, void* out, long ntok, int D, long V,
+                             hipStream_t s) {
+  if (D % 8) return hipErrorInvalidValue;
+  const int grid = (int)((ntok + 3) / 4);
+  PRA_DISPATCH_FLOAT(dtype, T,
+                     hipLaunchKernelGGL((pra::embed_fwd_kernel<T>), dim3(grid), dim3(256), 0, s, ids, (const T*)W,
+                                        (T*)out, ntok, D, V));
+  return hipGetLastError();
+}
+
+hipError_t pra_embedding_bwd(int dtype, const int64_t* sorted_ids, const int64_t* perm, const void* dout,
+                             void* dW, long ntok, int D, long V, int accumulate, hipStream_t s) {
+  if (D % 8) return hipErrorInvalidValue;
+  const int grid = (int)((ntok + 3) / 4);
+  PRA_DISPATCH_FLOAT(dtype, T,
+                     hipLaunchKernelGGL((pra::embed_bwd_kernel<T>), dim3(grid), dim3(256), 0, s, sorted_ids, perm,
+                                        (const T*)dout, (T*)dW, ntok, D, V, accumulate));
+  return hipGetLastError();
+}
+
+}  // extern "C"

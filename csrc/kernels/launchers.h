@@ -1,0 +1,45 @@
+// C ABI of the HIP kernels in csrc/kernels/*.hip. The kernel translation units do not include
+// any torch header; csrc/bindings.cpp adapts torch tensors to these raw-pointer launchers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+extern "C" {
+int pra_rmsnorm_bwd_ws_rows(int rows);
+hipError_t pra_rmsnorm_fwd(int dtype, const void* x, const void* delta, const void* w, void* h_out, void* y,
+                           float* rstd, int rows, int D, float eps, hipStream_t s);
+hipError_t pra_rmsnorm_bwd(int dtype, const void* dy, const void* h, const void* w, const float* rstd,
+                           const void* dres, void* dx, void* dw, float* ws, int rows, int D, int accumulate,
+                           hipStream_t s);
+
+hipError_t pra_rope(int dtype, void* x, const void* tab, long ntok, int ld, int ncols, int D, int S,
+                    int pos_offset, int inverse, hipStream_t s);
+hipError_t pra_swiglu_fwd(int dtype, const void* g, const void* u, void* y, long ntok, int F, int ldg, int ldu,
+                          int ldy, hipStream_t s);
+hipError_t pra_swiglu_bwd(int dtype, const void* dy, const void* g, const void* u, void* dg, void* du, long ntok,
+                          int F, int ldg, int ldu, int lddy, hipStream_t s);
+hipError_t pra_embedding_fwd(int dtype, const int64_t* ids, const void* W, void* out, long ntok, int D, long V,
+                             hipStream_t s);
+hipError_t pra_embedding_bwd(int dtype, const int64_t* sorted_ids, const int64_t* perm, const void* dout, void* dW,
+                             long ntok, int D, long V, int accumulate, hipStream_t s);
+
+hipError_t pra_xent_fwd(int dtype, const void* logits, const int64_t* labels, float* lse, float* loss_row,
+                        float* stats, long T, long V, long ld, long ignore_index, hipStream_t s);
+hipError_t pra_xent_bwd(int dtype, void* logits, const int64_t* labels, const float* lse, const float* stats,
+                        const float* grad_out, long T, long V, long ld, long ignore_index, hipStream_t s);
+
+hipError_t pra_adamw_flat(int pdtype, int sdtype, void* p, const void* g, void* m, void* v, long n, float lr,
+                          float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt, float gscale,
+                          const float* gscale_dev, hipStream_t s);
+int pra_sumsq_partials();
+hipError_t pra_grad_norm(int dtype, const void* x, long n, float* ws, float* out, float max_norm, float pre_scale,
+                         hipStream_t s);
+
+hipError_t pra_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int Hq,
+                        int Hkv, int D, long ldq, long ldk, long ldv, long ldo, float scale, int causal,
+                        hipStream_t st);
+hipError_t pra_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                        const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int S, int Hq, int Hkv,
+                        int D, long ldq, long ldk, long ldv, long ldo, long lddo, long lddq, long lddk, long lddv,
+                        float scale, int causal, hipStream_t st);
+}

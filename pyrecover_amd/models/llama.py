@@ -1,0 +1,199 @@
+"""Llama-style decoder with the reference's parameter names, shapes, order and init.
+
+Module tree and state-dict keys are identical to reference model.py:330-395
+(``tok_embeddings``, ``layers.{i}.attention.{wq,wk,wv,wo}``, ``layers.{i}.feed_forward.{w1,w2,w3}``,
+``layers.{i}.{attention_norm,ffn_norm}``, ``norm``, ``output``; ``freqs_cis`` is a non-persistent
+buffer), and parameters are created in the same order with the same ``nn.Linear`` /
+``nn.Embedding`` initializers, so a seeded CPU construction is bit-identical to the reference's.
+
+The forward is NOT the reference's module-by-module composition: it runs the fused ops of
+:mod:`pyrecover_amd.ops` (fused residual-add + RMSNorm, fused QKV GEMM + in-place RoPE + HIP flash
+attention with native GQA, fused W1|W3 GEMM + SwiGLU, fused output GEMM + cross-entropy), and
+after :meth:`Transformer.flatten_` all parameters/gradients live in flat buffers
+(:mod:`pyrecover_amd.parallel.flat`).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+
+from ..config import TransformerModelArgs
+from ..ops import fused as F
+from ..ops.reference import precompute_freqs_cis, rope_table
+from ..parallel.flat import FlatParams
+
+
+class RMSNorm(nn.Module):
+    """Parameter container + reference-compatible eager forward (reference model.py:25-49)."""
+
+    def __init__(self, dim: int, eps: float = 1e-6):
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(dim))
+
+    def forward(self, x):
+        xf = x.float()
+        return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + self.eps)).type_as(x) * self.weight
+
+
+class Attention(nn.Module):
+    def __init__(self, args: TransformerModelArgs):
+        super().__init__()
+        self.n_heads = args.n_heads
+        self.n_kv_heads = args.kv_heads
+        self.n_rep = self.n_heads // self.n_kv_heads
+        self.head_dim = args.dim // args.n_heads
+        self.wq = nn.Linear(args.dim, args.n_heads * self.head_dim, bias=False)
+        self.wk = nn.Linear(args.dim, self.n_kv_heads * self.head_dim, bias=False)
+        self.wv = nn.Linear(args.dim, self.n_kv_heads * self.head_dim, bias=False)
+        self.wo = nn.Linear(args.n_heads * self.head_dim, args.dim, bias=False)
+        self.use_flash_attention = args.use_flash_attention  # accepted for CLI parity; HIP flash always used on GPU
+
+
+class FeedForward(nn.Module):
+    def __init__(self, dim: int, hidden_dim: int, multiple_of: int, ffn_dim_multiplier: Optional[float]):
+        super().__init__()
+        hidden_dim = int(2 * hidden_dim / 3)
+        if ffn_dim_multiplier is not None:
+            hidden_dim = int(ffn_dim_multiplier * hidden_dim)
+        hidden_dim = multiple_of * ((hidden_dim + multiple_of - 1) // multiple_of)
+        self.w1 = nn.Linear(dim, hidden_dim, bias=False)
+        self.w2 = nn.Linear(hidden_dim, dim, bias=False)
+        self.w3 = nn.Linear(dim, hidden_dim, bias=False)
+
+
+class TransformerBlock(nn.Module):
+    def __init__(self, layer_id: int, args: TransformerModelArgs):
+        super().__init__()
+        self.n_heads = args.n_heads
+        self.dim = args.dim
+        self.attention = Attention(args)
+        self.feed_forward = FeedForward(args.dim, 4 * args.dim, args.multiple_of, args.ffn_dim_multiplier)
+        self.layer_id = layer_id
+        self.num_layers = args.n_layers
+        self.attention_norm = RMSNorm(args.dim, eps=args.norm_eps)
+        self.ffn_norm = RMSNorm(args.dim, eps=args.norm_eps)
+
+
+class Transformer(nn.Module):
+    def __init__(self, model_args: TransformerModelArgs):
+        super().__init__()
+        if model_args.vocab_size <= 0:
+            raise ValueError("vocab_size must be set")
+        self.model_args = model_args
+        self.vocab_size = model_args.vocab_size
+        self.n_layers = model_args.n_layers
+        self.tok_embeddings = nn.Embedding(model_args.vocab_size, model_args.dim)
+        self.register_buffer("freqs_cis", self._precompute_freqs_cis(), persistent=False)
+        self.layers = nn.ModuleDict()
+        for layer_id in range(model_args.n_layers):
+            self.layers[str(layer_id)] = TransformerBlock(layer_id, model_args)
+        self.norm = RMSNorm(model_args.dim, eps=model_args.norm_eps)
+        self.output = nn.Linear(model_args.dim, model_args.vocab_size, bias=False)
+        self.register_buffer("rope_tab", rope_table(self.freqs_cis), persistent=False)
+        self.flat: Optional[FlatParams] = None
+
+    def _precompute_freqs_cis(self) -> torch.Tensor:
+        a = self.model_args
+        with torch.device("cpu"):
+            fc = precompute_freqs_cis(a.dim // a.n_heads, a.seq_len, a.rope_theta)
+        return fc
+
+    def _apply(self, fn, recurse=True):
+        out = super()._apply(fn, recurse)
+        # the rotation table always stays fp32 (it is a non-persistent buffer)
+        if self.rope_tab.dtype != torch.float32:
+            self.rope_tab = rope_table(self.freqs_cis.to(self.rope_tab.device))
+        if self.flat is not None and any(p.data.data_ptr() < self.flat.data.data_ptr() or
+                                         p.data.data_ptr() >= self.flat.data.data_ptr() + self.flat.state_bytes()
+                                         for p in self.parameters()):
+            self.flat = None  # a .to()/.half() replaced the storages: flat views are gone
+        return out
+
+    # ----------------------------------------------------------------------------------
+    def fusion_groups(self) -> List[List[Tuple[str, nn.Parameter]]]:
+        """Flat-buffer layout in forward order (gradients become ready in reverse order, so DDP
+        buckets are contiguous tail-first slices). Adjacent members form fused GEMM weights."""
+        g = [[("tok_embeddings.weight", self.tok_embeddings.weight)]]
+        for i, layer in self.layers.items():
+            p = f"layers.{i}."
+            at, ff = layer.attention, layer.feed_forward
+            g.append([(p + "attention_norm.weight", layer.attention_norm.weight)])
+            g.append([(p + "attention.wq.weight", at.wq.weight), (p + "attention.wk.weight", at.wk.weight),
+                      (p + "attention.wv.weight", at.wv.weight)])
+            g.append([(p + "attention.wo.weight", at.wo.weight)])
+            g.append([(p + "ffn_norm.weight", layer.ffn_norm.weight)])
+            g.append([(p + "feed_forward.w1.weight", ff.w1.weight), (p + "feed_forward.w3.weight", ff.w3.weight)])
+            g.append([(p + "feed_forward.w2.weight", ff.w2.weight)])
+        g.append([("norm.weight", self.norm.weight)])
+        g.append([("output.weight", self.output.weight)])
+        return g
+
+    def flatten_(self) -> FlatParams:
+        """Move all parameters/gradients into flat buffers (call after the final .to(device/dtype))."""
+        if self.flat is None:
+            self.flat = FlatParams(self.fusion_groups())
+        return self.flat
+
+    # ----------------------------------------------------------------------------------
+    def _slot(self, params: Sequence[nn.Parameter]):
+        if self.flat is not None:
+            return F.FlatSlotAdapter(self.flat.slot(params[0]))
+        return F.UnflatSlot(params)
+
+    def _weight(self, params: Sequence[nn.Parameter]) -> torch.Tensor:
+        rows = sum(p.shape[0] for p in params)
+        if self.flat is not None:
+            return self.flat.weight(params, (rows, params[0].shape[1]))
+        if len(params) == 1:
+            return params[0].detach()
+        return torch.cat([p.detach() for p in params], 0)
+
+    def _trunk(self, tokens: torch.Tensor):
+        a = self.model_args
+        B, S = tokens.shape
+        if S > a.seq_len:
+            raise ValueError(f"sequence length {S} exceeds model seq_len {a.seq_len}")
+        dims = (B, S, a.n_heads, a.kv_heads, a.head_dim, True)
+        emb = self.tok_embeddings.weight
+        h = F.embedding(tokens, emb, self._slot([emb]))
+        pending = None
+        for layer in self.layers.values():
+            at, ff = layer.attention, layer.feed_forward
+            wn1 = layer.attention_norm.weight
+            if pending is None:
+                x, n1 = h, F.add_rms_norm(h, None, wn1, self._slot([wn1]), layer.attention_norm.eps)
+            else:
+                x, n1 = F.add_rms_norm(h, pending, wn1, self._slot([wn1]), layer.attention_norm.eps)
+            qkv_p = [at.wq.weight, at.wk.weight, at.wv.weight]
+            att = F.attention_block(n1, self._weight(qkv_p), self._weight([at.wo.weight]), self._slot(qkv_p),
+                                    self._slot([at.wo.weight]), self.rope_tab, dims, qkv_p + [at.wo.weight])
+            wn2 = layer.ffn_norm.weight
+            x2, n2 = F.add_rms_norm(x, att, wn2, self._slot([wn2]), layer.ffn_norm.eps)
+            up = [ff.w1.weight, ff.w3.weight]
+            mlp = F.swiglu_mlp(n2, self._weight(up), self._weight([ff.w2.weight]), self._slot(up),
+                               self._slot([ff.w2.weight]), up + [ff.w2.weight])
+            h, pending = x2, mlp
+        wn = self.norm.weight
+        if pending is None:
+            return F.add_rms_norm(h, None, wn, self._slot([wn]), self.norm.eps)
+        _, nf = F.add_rms_norm(h, pending, wn, self._slot([wn]), self.norm.eps)
+        return nf
+
+    def forward(self, tokens: torch.Tensor, labels: Optional[torch.Tensor] = None, ignore_index: int = -100):
+        """logits (B, S, V) like the reference, or the mean causal-LM loss when labels are given
+        (fused output GEMM + cross-entropy, equal to reference train.py:263-266)."""
+        nf = self._trunk(tokens)
+        W = self.output.weight
+        if labels is not None:
+            return F.linear_cross_entropy(nf, self._weight([W]), labels, self._slot([W]), W, ignore_index)
+        return torch.nn.functional.linear(nf, W)
+
+    # ----------------------------------------------------------------------------------
+    def num_params(self, exclude_embedding: bool = False) -> int:
+        n = sum(p.numel() for p in self.parameters())
+        if exclude_embedding:
+            n -= self.tok_embeddings.weight.numel()
+        return n

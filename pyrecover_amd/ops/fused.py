@@ -1,0 +1,359 @@
+"""Fused autograd ops of the Transformer hot path.
+
+Each op runs the HIP kernels of ``pyrecover_amd._C`` for GPU tensors and the plain-torch math of
+:mod:`pyrecover_amd.ops.reference` for CPU tensors (CPU/gloo runs only). GEMMs are plain
+library GEMMs (``torch.mm`` -> hipBLASLt on ROCm); everything between them is ours.
+
+Weight gradients are produced directly into *gradient slots* (:mod:`pyrecover_amd.parallel.flat`)
+instead of being returned to autograd, so they land in the flat gradient buffer / DDP bucket
+without an AccumulateGrad pass. The parameters are still passed as inputs so autograd knows the
+graph depends on them; their returned gradient is ``None``.
+
+Reference parity (reference model.py): embedding (:355,388), RMSNorm (:25-49) with the residual
+adds of TransformerBlock.forward (:325-327), Attention.forward (:194-230: QKV projections, RoPE,
+causal SDPA with GQA, output projection), FeedForward.forward (:268-269), the output head
+(:367,394) and the loss of train.py:263-266.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Sequence, Tuple
+
+import torch
+
+from .. import _ext
+from . import reference as ref
+
+
+# ---------------------------------------------------------------------------------------
+# gradient slots for modules that are not (yet) flattened
+class UnflatSlot:
+    """Gradient sink that accumulates into ``p.grad`` for a group of adjacent params."""
+
+    def __init__(self, params: Sequence[torch.nn.Parameter]):
+        self.params = list(params)
+        self.numel = sum(p.numel() for p in self.params)
+
+    def begin(self, like: torch.Tensor):
+        return torch.empty(self.numel, dtype=self.params[0].dtype, device=self.params[0].device), False
+
+    def end(self, buf: torch.Tensor):
+        o = 0
+        for p in self.params:
+            part = buf[o:o + p.numel()].view_as(p)
+            if p.grad is None:
+                p.grad = part.clone()
+            else:
+                p.grad.add_(part)
+            o += p.numel()
+
+    def mm_(self, a, b, shape):
+        buf, _ = self.begin(a)
+        torch.mm(a, b, out=buf.view(shape))
+        self.end(buf)
+
+
+class FlatSlotAdapter:
+    """begin/end protocol over a :class:`~pyrecover_amd.parallel.flat.GradSlot`."""
+
+    __slots__ = ("s",)
+
+    def __init__(self, s):
+        self.s = s
+
+    def begin(self, like):
+        return self.s.view, self.s.take()
+
+    def end(self, buf):
+        self.s.done()
+
+    def mm_(self, a, b, shape):
+        self.s.mm_(a, b, shape)
+
+
+def _mm_into(slot, a, b, shape):
+    slot.mm_(a, b, shape)
+
+
+# ---------------------------------------------------------------------------------------
+class _Embedding(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, weight, slot):
+        ctx.slot = slot
+        ctx.save_for_backward(ids)
+        ctx.shape = weight.shape
+        if weight.is_cuda:
+            return _ext.require_for(weight).embedding_fwd(ids.contiguous(), weight)
+        return torch.nn.functional.embedding(ids, weight)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (ids,) = ctx.saved_tensors
+        slot = ctx.slot
+        buf, acc = slot.begin(dout)
+        V, D = ctx.shape
+        if dout.is_cuda:
+            _ext.require_for(dout).embedding_bwd(ids.contiguous(), dout.contiguous(), buf.view(V, D), acc)
+        else:
+            g = buf.view(V, D)
+            if not acc:
+                g.zero_()
+            g.index_add_(0, ids.reshape(-1), dout.reshape(-1, D).to(g.dtype))
+        slot.end(buf)
+        return None, None, None
+
+
+def embedding(ids, weight, slot):
+    return _Embedding.apply(ids, weight, slot)
+
+
+# ---------------------------------------------------------------------------------------
+class _AddRMSNorm(torch.autograd.Function):
+    """(h, y) = (x + delta, rmsnorm(x + delta) * w); delta may be None (then h is x)."""
+
+    @staticmethod
+    def forward(ctx, x, delta, weight, slot, eps):
+        ctx.slot = slot
+        ctx.has_delta = delta is not None
+        if x.is_cuda:
+            h, y, rstd = _ext.require_for(x).rmsnorm_fwd(x.contiguous(), delta.contiguous() if delta is not None else None,
+                                                         weight, eps)
+        else:
+            h, y, rstd = ref.rmsnorm_fwd(x, delta, weight, eps)
+        ctx.save_for_backward(h, weight, rstd)
+        if delta is None:
+            return y
+        return h, y
+
+    @staticmethod
+    def backward(ctx, *grads):
+        h, weight, rstd = ctx.saved_tensors
+        if ctx.has_delta:
+            dh, dy = grads
+        else:
+            dh, dy = None, grads[0]
+        slot = ctx.slot
+        buf, acc = slot.begin(dy)
+        if dy.is_cuda:
+            dx = _ext.require_for(dy).rmsnorm_bwd(dy.contiguous(), h, weight, rstd,
+                                                  dh.contiguous() if dh is not None else None, buf, acc)
+        else:
+            dx, dw = ref.rmsnorm_bwd(dy, h, weight, rstd, dh)
+            if acc:
+                buf.add_(dw.to(buf.dtype))
+            else:
+                buf.copy_(dw)
+        slot.end(buf)
+        if ctx.has_delta:
+            return dx, dx, None, None, None
+        return dx, None, None, None, None
+
+
+def add_rms_norm(x, delta, weight, slot, eps):
+    """Returns (h, normed) when delta is given, else normed."""
+    return _AddRMSNorm.apply(x, delta, weight, slot, eps)
+
+
+# ---------------------------------------------------------------------------------------
+def _attn_fwd(q, k, v, scale, causal):
+    if q.is_cuda:
+        return _ext.require_for(q).attn_fwd(q, k, v, scale, causal)
+    o, lse = ref.attention_lse_ref(q, k, v, causal, scale)
+    return o.to(q.dtype).contiguous(), lse
+
+
+def _attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, causal):
+    if q.is_cuda:
+        _ext.require_for(q).attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, causal)
+        return
+    with torch.enable_grad():
+        qq, kk, vv = (t.detach().float().requires_grad_() for t in (q, k, v))
+        out, _ = ref.attention_lse_ref(qq, kk, vv, causal, scale)
+        gq, gk, gv = torch.autograd.grad(out, (qq, kk, vv), do.float())
+    dq.copy_(gq)
+    dk.copy_(gk)
+    dv.copy_(gv)
+
+
+class _AttentionBlock(torch.autograd.Function):
+    """y = Wo · attn(rope(Wq x), rope(Wk x), Wv x) with a fused QKV GEMM."""
+
+    @staticmethod
+    def forward(ctx, x, w_qkv, w_o, slot_qkv, slot_o, tab, dims, *params):
+        B, S, Hq, Hkv, D, causal = dims
+        T = B * S
+        dim = x.shape[-1]
+        x2 = x.reshape(T, dim)
+        qkv = torch.mm(x2, w_qkv.t())
+        nq, nk = Hq * D, Hkv * D
+        if qkv.is_cuda:
+            _ext.require_for(qkv).rope_(qkv, nq + nk, tab, D, S, 0, False)
+        else:
+            ref.rope_inplace_2d(qkv, nq + nk, tab, D, S)
+        q = qkv[:, :nq].view(B, S, Hq, D)
+        k = qkv[:, nq:nq + nk].view(B, S, Hkv, D)
+        v = qkv[:, nq + nk:].view(B, S, Hkv, D)
+        scale = 1.0 / math.sqrt(D)
+        o, lse = _attn_fwd(q, k, v, scale, causal)
+        o2 = o.view(T, nq)
+        y = torch.mm(o2, w_o.t())
+        ctx.save_for_backward(x2, qkv, o, lse, w_qkv, w_o, tab)
+        ctx.slots = (slot_qkv, slot_o)
+        ctx.dims = dims
+        ctx.scale = scale
+        return y.view(B, S, dim)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, qkv, o, lse, w_qkv, w_o, tab = ctx.saved_tensors
+        slot_qkv, slot_o = ctx.slots
+        B, S, Hq, Hkv, D, causal = ctx.dims
+        T = B * S
+        nq, nk = Hq * D, Hkv * D
+        dy2 = dy.reshape(T, -1)
+        o2 = o.view(T, nq)
+        slot_o.mm_(dy2.t(), o2, tuple(w_o.shape))
+        do = torch.mm(dy2, w_o).view(B, S, Hq, D)
+        dqkv = torch.empty_like(qkv)
+        q = qkv[:, :nq].view(B, S, Hq, D)
+        k = qkv[:, nq:nq + nk].view(B, S, Hkv, D)
+        v = qkv[:, nq + nk:].view(B, S, Hkv, D)
+        dq = dqkv[:, :nq].view(B, S, Hq, D)
+        dk = dqkv[:, nq:nq + nk].view(B, S, Hkv, D)
+        dv = dqkv[:, nq + nk:].view(B, S, Hkv, D)
+        _attn_bwd(q, k, v, o, do, lse, dq, dk, dv, ctx.scale, causal)
+        if dqkv.is_cuda:
+            _ext.require_for(dqkv).rope_(dqkv, nq + nk, tab, D, S, 0, True)
+        else:
+            ref.rope_inplace_2d(dqkv, nq + nk, tab, D, S, inverse=True)
+        slot_qkv.mm_(dqkv.t(), x2, tuple(w_qkv.shape))
+        dx = torch.mm(dqkv, w_qkv)
+        n_params = ctx.needs_input_grad.__len__() - 7
+        return (dx.view(B, S, -1), None, None, None, None, None, None) + (None,) * n_params
+
+
+def attention_block(x, w_qkv, w_o, slot_qkv, slot_o, tab, dims, params):
+    return _AttentionBlock.apply(x, w_qkv, w_o, slot_qkv, slot_o, tab, dims, *params)
+
+
+# ---------------------------------------------------------------------------------------
+def _swiglu_fwd(gu):
+    if gu.is_cuda:
+        return _ext.require_for(gu).swiglu_fwd(gu)
+    F = gu.shape[1] // 2
+    g, u = gu[:, :F].float(), gu[:, F:].float()
+    return (torch.nn.functional.silu(g).to(gu.dtype).float() * u).to(gu.dtype)
+
+
+def _swiglu_bwd_(da, gu):
+    if gu.is_cuda:
+        return _ext.require_for(gu).swiglu_bwd(da, gu, gu)
+    F = gu.shape[1] // 2
+    dg, du = ref.swiglu_bwd_ref(da, gu[:, :F], gu[:, F:])
+    gu[:, :F] = dg
+    gu[:, F:] = du
+    return gu
+
+
+class _SwiGLUMLP(torch.autograd.Function):
+    """y = W2 (silu(W1 x) * (W3 x)) with W1|W3 fused into one GEMM."""
+
+    @staticmethod
+    def forward(ctx, x, w13, w2, slot13, slot2, *params):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        gu = torch.mm(x2, w13.t())
+        a = _swiglu_fwd(gu)
+        y = torch.mm(a, w2.t())
+        ctx.save_for_backward(x2, gu, a, w13, w2)
+        ctx.slots = (slot13, slot2)
+        return y.view(shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, gu, a, w13, w2 = ctx.saved_tensors
+        slot13, slot2 = ctx.slots
+        shape = dy.shape
+        dy2 = dy.reshape(-1, shape[-1])
+        slot2.mm_(dy2.t(), a, tuple(w2.shape))
+        da = torch.mm(dy2, w2)
+        dgu = _swiglu_bwd_(da, gu)  # in place over gu (dead after this)
+        slot13.mm_(dgu.t(), x2, tuple(w13.shape))
+        dx = torch.mm(dgu, w13)
+        n_params = len(ctx.needs_input_grad) - 5
+        return (dx.view(shape), None, None, None, None) + (None,) * n_params
+
+
+def swiglu_mlp(x, w13, w2, slot13, slot2, params):
+    return _SwiGLUMLP.apply(x, w13, w2, slot13, slot2, *params)
+
+
+# ---------------------------------------------------------------------------------------
+class _LinearCrossEntropy(torch.autograd.Function):
+    """loss = CE(h · Wout^T, labels, sum) / #valid; logits never leave bf16 and are turned into
+    dlogits in place during the backward."""
+
+    @staticmethod
+    def forward(ctx, h, w_out, labels, slot, ignore_index, weight_param):
+        h2 = h.reshape(-1, h.shape[-1])
+        lab = labels.reshape(-1).contiguous()
+        logits = torch.mm(h2, w_out.t())
+        if logits.is_cuda:
+            lse, _, stats = _ext.require_for(logits).xent_fwd(logits, lab, ignore_index)
+            loss = stats[0]
+        else:
+            lf = logits.float()
+            lse = torch.logsumexp(lf, dim=-1)
+            stats = None
+            loss = ref.cross_entropy_ref(logits, lab, ignore_index)
+        ctx.save_for_backward(h2, logits, lab, lse, w_out, stats if stats is not None else lse)
+        ctx.slot = slot
+        ctx.ignore_index = ignore_index
+        ctx.hshape = h.shape
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        h2, logits, lab, lse, w_out, stats = ctx.saved_tensors
+        if logits.is_cuda:
+            g = dloss.reshape(1).float().contiguous()
+            _ext.require_for(logits).xent_bwd_(logits, lab, lse, stats, g, ctx.ignore_index)
+            dlogits = logits
+        else:
+            valid = lab.ne(ctx.ignore_index)
+            n = valid.sum().clamp_min(1)
+            p = torch.softmax(logits.float(), dim=-1)
+            p[torch.arange(lab.numel()), lab.clamp_min(0)] -= valid.float()
+            p = p * valid.float().unsqueeze(1) * (dloss.float() / n)
+            dlogits = p.to(logits.dtype)
+        ctx.slot.mm_(dlogits.t(), h2, tuple(w_out.shape))
+        dh = torch.mm(dlogits, w_out)
+        return dh.view(ctx.hshape), None, None, None, None, None
+
+
+def linear_cross_entropy(h, w_out, labels, slot, weight_param, ignore_index: int = -100):
+    return _LinearCrossEntropy.apply(h, w_out, labels, slot, ignore_index, weight_param)
+
+
+# ---------------------------------------------------------------------------------------
+# Standalone user-facing ops (autograd, no slots)
+class _FlashAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale):
+        o, lse = _attn_fwd(q, k, v, scale, causal)
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.causal, ctx.scale = causal, scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        _attn_bwd(q, k, v, o, do.contiguous(), lse, dq, dk, dv, ctx.scale, ctx.causal)
+        return dq, dk, dv, None, None
+
+
+def flash_attention(q, k, v, causal: bool = True, scale: Optional[float] = None):
+    """Causal/full GQA attention on [B, S, H, D] tensors (HIP MFMA kernel on GPU)."""
+    scale = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
+    return _FlashAttention.apply(q, k, v, causal, scale)

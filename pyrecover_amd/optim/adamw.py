@@ -1,0 +1,128 @@
+"""AdamW over the flat parameter space, state_dict-compatible with ``torch.optim.AdamW``.
+
+The reference builds ``torch.optim.AdamW(model.parameters(), lr, fused=--fused-optimizer)``
+(reference train.py:120-122) with default betas/eps/weight_decay on all params and bf16 states
+(no fp32 master copy). :class:`FlatAdamW` keeps that contract (same param_groups keys, per-param
+``state[i] = {"step", "exp_avg", "exp_avg_sq"}`` in ``model.parameters()`` order), but the moments
+live in two flat buffers laid out like the flat parameters, and the update is one HIP kernel
+over the whole model (``pra_adamw_flat``: fp32 opmath, torch ``_fused_adamw_`` semantics).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from .. import _ext
+from ..parallel.flat import FlatParams
+
+
+class FlatAdamW(torch.optim.AdamW):
+    def __init__(self, flat: FlatParams, params=None, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 1e-2, fused: Optional[bool] = None, grad_scale: float = 1.0):
+        params = list(params) if params is not None else list(flat.params)
+        for p in params:
+            if id(p) not in flat.param_offset:
+                raise ValueError("every optimized parameter must live in the flat buffer")
+        # fused=None keeps torch from validating device support for the CPU path; the flag is
+        # recorded in param_groups for state_dict parity with the reference.
+        super().__init__(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        for g in self.param_groups:
+            g["fused"] = bool(fused)
+        if len(self.param_groups) != 1:
+            raise ValueError("FlatAdamW supports a single param group (the reference uses one)")
+        self.flat = flat
+        self.grad_scale = grad_scale  # e.g. 1/world_size after a SUM all-reduce
+        self.grad_scale_dev: Optional[torch.Tensor] = None  # device-side multiplier (clipping)
+        self.exp_avg = torch.zeros_like(flat.data)
+        self.exp_avg_sq = torch.zeros_like(flat.data)
+        self._step = 0
+        self._bind_state()
+
+    def _bind_state(self):
+        for p in self.param_groups[0]["params"]:
+            o = self.flat.param_offset[id(p)]
+            n = p.numel()
+            self.state[p] = {
+                "step": torch.tensor(float(self._step), dtype=torch.float32),
+                "exp_avg": self.exp_avg[o:o + n].view_as(p),
+                "exp_avg_sq": self.exp_avg_sq[o:o + n].view_as(p),
+            }
+
+    # --- torch.optim.Optimizer API ------------------------------------------------------
+    def zero_grad(self, set_to_none: bool = True):
+        """Marks gradient slots fresh; the flat gradient views are never set to None."""
+        self.flat.zero_grad()
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        g = self.param_groups[0]
+        self._step += 1
+        b1, b2 = g["betas"]
+        lr, eps, wd = float(g["lr"]), float(g["eps"]), float(g["weight_decay"])
+        bc1 = 1.0 - b1 ** self._step
+        bc2_sqrt = math.sqrt(1.0 - b2 ** self._step)
+        f = self.flat
+        if f.data.is_cuda:
+            _ext.require_for(f.data).adamw_flat_(f.data, f.grad, self.exp_avg, self.exp_avg_sq, lr, b1, b2, eps, wd,
+                                                 bc1, bc2_sqrt, self.grad_scale, self.grad_scale_dev)
+        else:
+            self._step_reference(lr, b1, b2, eps, wd, bc1, bc2_sqrt)
+        return loss
+
+    def _step_reference(self, lr, b1, b2, eps, wd, bc1, bc2_sqrt):
+        f = self.flat
+        gs = self.grad_scale * (float(self.grad_scale_dev[0]) if self.grad_scale_dev is not None else 1.0)
+        p = f.data.float()
+        gr = f.grad.float() * gs
+        m = self.exp_avg.float()
+        v = self.exp_avg_sq.float()
+        p.mul_(1 - lr * wd)
+        m.lerp_(gr, 1 - b1)
+        v.mul_(b2).addcmul_(gr, gr, value=1 - b2)
+        denom = v.sqrt().div_(bc2_sqrt).add_(eps)
+        p.addcdiv_(m, denom, value=-(lr / bc1))
+        f.data.copy_(p)
+        self.exp_avg.copy_(m)
+        self.exp_avg_sq.copy_(v)
+
+    # --- checkpoint compatibility -------------------------------------------------------
+    def state_dict(self):
+        for st in self.state.values():
+            st["step"] = torch.tensor(float(self._step), dtype=torch.float32)
+        return super().state_dict()
+
+    def load_state_dict(self, state_dict):
+        """Accepts torch.optim.AdamW state dicts (ours or the reference's)."""
+        groups = state_dict["param_groups"]
+        if len(groups) != 1:
+            raise ValueError("expected exactly one param group")
+        params = self.param_groups[0]["params"]
+        saved_ids = groups[0]["params"]
+        if len(saved_ids) != len(params):
+            raise ValueError(f"optimizer state has {len(saved_ids)} params, model has {len(params)}")
+        for k, v in groups[0].items():
+            if k != "params":
+                self.param_groups[0][k] = v
+        steps = set()
+        with torch.no_grad():
+            for sid, p in zip(saved_ids, params):
+                st = state_dict["state"].get(sid, state_dict["state"].get(str(sid)))
+                mine = self.state[p]
+                if st is None:
+                    mine["exp_avg"].zero_()
+                    mine["exp_avg_sq"].zero_()
+                    continue
+                mine["exp_avg"].copy_(st["exp_avg"])
+                mine["exp_avg_sq"].copy_(st["exp_avg_sq"])
+                steps.add(float(st["step"]))
+        if len(steps) > 1:
+            raise ValueError(f"inconsistent per-parameter step counts {sorted(steps)}")
+        self._step = int(steps.pop()) if steps else 0
+        for st in self.state.values():
+            st["step"] = torch.tensor(float(self._step), dtype=torch.float32)

@@ -1,0 +1,131 @@
+"""Process-group runtime: SLURM / torchrun / single-process detection, device binding.
+
+Function names mirror reference dist_utils.py (``maybe_init_distributed``, ``get_rank``,
+``is_rank0``, ``is_distributed_activated``, ``log_rank0``, ``maybe_cleanup_distributed``,
+``get_slurm_job_end_time_env``; reference dist_utils.py:14-101) but the runtime also accepts
+torchrun-style env (RANK/WORLD_SIZE/LOCAL_RANK), picks RCCL (torch backend "nccl" on ROCm) on GPU
+and gloo on CPU, and never calls ``exit()`` on a bad environment (it raises).
+
+One process per GPU; the collective layer for gradients is RCCL over xGMI.
+"""
+from __future__ import annotations
+
+import datetime
+import logging
+import os
+from typing import Optional, Tuple
+
+import torch
+
+logger = logging.getLogger("pyrecover")
+
+_STATE = {"rank": 0, "world": 1, "local_rank": 0, "initialized": False, "backend": None}
+
+
+def is_distributed_slurm_env() -> bool:
+    return "SLURM_PROCID" in os.environ and int(os.environ.get("SLURM_NTASKS", "1")) > 1
+
+
+def is_torchrun_env() -> bool:
+    return "RANK" in os.environ and "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) >= 1
+
+
+def is_distributed_activated() -> bool:
+    return "DISTRIBUTED_RUN" in os.environ
+
+
+def _env_rank_world_local() -> Optional[Tuple[int, int, int]]:
+    if is_torchrun_env() and int(os.environ["WORLD_SIZE"]) > 1:
+        return int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"]), int(os.environ.get("LOCAL_RANK", 0))
+    if is_distributed_slurm_env():
+        return (int(os.environ["SLURM_PROCID"]), int(os.environ["SLURM_NTASKS"]),
+                int(os.environ.get("SLURM_LOCALID", 0)))
+    return None
+
+
+def get_rank() -> int:
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        return torch.distributed.get_rank()
+    return 0
+
+
+def get_world_size() -> int:
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        return torch.distributed.get_world_size()
+    return 1
+
+
+def is_rank_eq(rank: int) -> bool:
+    return get_rank() == rank
+
+
+def is_rank0() -> bool:
+    return get_rank() == 0
+
+
+def local_rank() -> int:
+    return _STATE["local_rank"]
+
+
+def maybe_init_distributed(activate_distributed: bool, backend: Optional[str] = None,
+                           timeout_s: float = 1800.0) -> Tuple[int, int]:
+    """Returns (local_rank, world_size). Initializes the process group when a multi-process
+    environment is present (SLURM with >1 tasks, or torchrun with WORLD_SIZE>1)."""
+    env = _env_rank_world_local()
+    if activate_distributed:
+        os.environ["DISTRIBUTED_RUN"] = "1"
+    if env is None:
+        if activate_distributed:
+            raise RuntimeError("--distributed was given but no multi-process SLURM/torchrun environment was found")
+        if torch.cuda.is_available():
+            torch.cuda.set_device(0)
+        return 0, 1
+    rank, world, lrank = env
+    os.environ["DISTRIBUTED_RUN"] = "1"
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29500")
+    use_gpu = torch.cuda.is_available()
+    if backend is None:
+        backend = "nccl" if use_gpu else "gloo"  # "nccl" is RCCL on ROCm
+    if use_gpu:
+        torch.cuda.set_device(lrank)
+    if not torch.distributed.is_initialized():
+        kw = {}
+        if backend == "nccl":
+            kw["device_id"] = torch.device("cuda", lrank)
+        torch.distributed.init_process_group(backend=backend, rank=rank, world_size=world,
+                                             timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    _STATE.update(rank=rank, world=world, local_rank=lrank, initialized=True, backend=backend)
+    log_rank0(f"Distributed initialized: backend={backend} world_size={world} rank={rank} local_rank={lrank}")
+    return lrank, world
+
+
+def maybe_cleanup_distributed():
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+def barrier():
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        torch.distributed.barrier()
+
+
+def log_rank(msg, rank):
+    if is_rank_eq(rank):
+        logger.info(msg)
+
+
+def log_rank0(msg):
+    log_rank(msg, 0)
+
+
+def get_slurm_job_end_time_env() -> Optional[float]:
+    """SLURM_JOB_END_TIME (UNIX seconds) or None (reference dist_utils.py:93-101)."""
+    val = os.environ.get("SLURM_JOB_END_TIME")
+    if val is not None:
+        try:
+            return float(val)
+        except ValueError:
+            pass
+    return None

@@ -1,0 +1,156 @@
+"""Flat parameter / gradient space.
+
+MI355X-first replacement for the per-tensor parameter handling that the reference gets from
+``nn.Module`` + ``DistributedDataParallel`` (reference train.py:107-122): every trainable
+parameter lives in ONE contiguous device buffer, every gradient in a second one with the same
+layout. Consequences:
+
+* fused GEMMs: adjacent parameters (wq|wk|wv, w1|w3) form one weight matrix view, so QKV and
+  the SwiGLU up-projection are single hipBLASLt GEMMs, and their weight gradients are written by
+  one GEMM straight into the flat gradient buffer (no AccumulateGrad copy, no grad zeroing pass);
+* DDP buckets are contiguous slices of the gradient buffer, all-reduced in place (no bucket
+  copy-in/copy-out);
+* the optimizer is one streaming kernel over four flat buffers (param/grad/m/v);
+* checkpoint snapshots are a handful of large D2H copies.
+
+Parameters keep their identity and names: ``p.data`` and ``p.grad`` are re-pointed to views of
+the flat buffers, so ``model.state_dict()`` / ``model.parameters()`` are unchanged.
+
+Gradient write protocol: each fusion group owns a :class:`GradSlot`. ``zero_grad()`` marks all
+slots *fresh* (no memory traffic); the first producer of a step overwrites (beta=0 GEMM), later
+producers (gradient accumulation) add. Parameters not covered by a fused op get ordinary
+autograd accumulation into their (zeroed) view and report readiness through a
+post-accumulate-grad hook.
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+ALIGN = 64  # elements; every group starts 128-B aligned for bf16 (16-B vector loads need 8)
+
+
+class GradSlot:
+    __slots__ = ("flat", "index", "params", "offset", "numel", "view", "fresh", "bucket", "fused")
+
+    def __init__(self, flat, index, params, offset, numel, fused):
+        self.flat = flat
+        self.index = index
+        self.params = params
+        self.offset = offset
+        self.numel = numel
+        self.view = flat.grad[offset:offset + numel]
+        self.fresh = True
+        self.bucket = -1
+        self.fused = fused
+
+    # --- producers ------------------------------------------------------------------
+    def mm_(self, a: torch.Tensor, b: torch.Tensor, shape: Tuple[int, int]):
+        """grad(slot) (+)= a @ b, written in place into the flat gradient buffer."""
+        out = self.view.view(shape)
+        if self.fresh:
+            torch.mm(a, b, out=out)
+            self.fresh = False
+        else:
+            out.addmm_(a, b)
+        self.flat._ready(self)
+
+    def take(self) -> bool:
+        """Claim the slot for a custom producer; returns True if it must accumulate."""
+        acc = not self.fresh
+        self.fresh = False
+        return acc
+
+    def done(self):
+        self.flat._ready(self)
+
+
+class FlatParams:
+    """Owns the flat parameter + gradient buffers for a list of fusion groups."""
+
+    def __init__(self, groups: Sequence[Sequence[Tuple[str, torch.nn.Parameter]]], fused_flags: Sequence[bool] = None,
+                 device=None, dtype=None):
+        flat_groups = [list(g) for g in groups if len(g)]
+        all_params = [p for g in flat_groups for _, p in g]
+        if len({id(p) for p in all_params}) != len(all_params):
+            raise ValueError("a parameter appears in more than one fusion group")
+        self.device = torch.device(device) if device is not None else all_params[0].device
+        self.dtype = dtype if dtype is not None else all_params[0].dtype
+        offs, off = [], 0
+        for g in flat_groups:
+            off = (off + ALIGN - 1) // ALIGN * ALIGN
+            offs.append(off)
+            off += sum(p.numel() for _, p in g)
+        self.numel = (off + ALIGN - 1) // ALIGN * ALIGN
+        self.data = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
+        self.grad = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
+        self.slots: List[GradSlot] = []
+        self.slot_of: Dict[int, GradSlot] = {}
+        self.param_offset: Dict[int, int] = {}
+        self.names: Dict[int, str] = {}
+        fused_flags = list(fused_flags) if fused_flags is not None else [True] * len(flat_groups)
+        with torch.no_grad():
+            for gi, (g, goff) in enumerate(zip(flat_groups, offs)):
+                o = goff
+                for name, p in g:
+                    n = p.numel()
+                    view = self.data[o:o + n].view_as(p)
+                    view.copy_(p.data)
+                    p.data = view
+                    p.grad = self.grad[o:o + n].view_as(p)
+                    self.param_offset[id(p)] = o
+                    self.names[id(p)] = name
+                    o += n
+                slot = GradSlot(self, gi, [p for _, p in g], goff, o - goff, fused_flags[gi])
+                self.slots.append(slot)
+                for _, p in g:
+                    self.slot_of[id(p)] = slot
+        self.params = all_params
+        self.reducer = None
+        self._hooks = []
+        for slot in self.slots:
+            if not slot.fused:
+                for p in slot.params:
+                    self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(slot)))
+        self._pending_unfused: Dict[int, int] = {}
+
+    # --- views ----------------------------------------------------------------------
+    def weight(self, params: Sequence[torch.nn.Parameter], shape: Tuple[int, int]) -> torch.Tensor:
+        """Contiguous weight view spanning adjacent params (e.g. wq|wk|wv)."""
+        o = self.param_offset[id(params[0])]
+        n = 0
+        for p in params:
+            if self.param_offset[id(p)] != o + n:
+                raise ValueError("fused params are not adjacent in the flat buffer")
+            n += p.numel()
+        return self.data[o:o + n].view(shape)
+
+    def slot(self, p: torch.nn.Parameter) -> GradSlot:
+        return self.slot_of[id(p)]
+
+    # --- step protocol ----------------------------------------------------------------
+    def zero_grad(self):
+        for s in self.slots:
+            s.fresh = True
+            if not s.fused:
+                s.view.zero_()
+                self._pending_unfused[s.index] = len(s.params)
+        if self.reducer is not None:
+            self.reducer.reset()
+
+    def _make_hook(self, slot: GradSlot) -> Callable:
+        def hook(p):
+            left = self._pending_unfused.get(slot.index, len(slot.params)) - 1
+            self._pending_unfused[slot.index] = left
+            slot.fresh = False
+            if left == 0:
+                self._ready(slot)
+        return hook
+
+    def _ready(self, slot: GradSlot):
+        if self.reducer is not None:
+            self.reducer.mark_ready(slot)
+
+    def state_bytes(self) -> int:
+        return self.numel * self.data.element_size()

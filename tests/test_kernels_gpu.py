@@ -1,0 +1,221 @@
+"""Numerics of every HIP kernel against a plain-PyTorch fp32 reference of the same op."""
+import math
+
+import pytest
+import torch
+
+from pyrecover_amd import _ext
+from pyrecover_amd.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-6)).item()
+
+
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("rows,D", [(333, 4096), (64, 768), (17, 128)])
+@pytest.mark.parametrize("with_delta", [False, True])
+def test_rmsnorm(cuda, rows, D, with_delta):
+    C = _ext.native()
+    torch.manual_seed(0)
+    x = torch.randn(rows, D, device=cuda, dtype=torch.bfloat16)
+    d = torch.randn(rows, D, device=cuda, dtype=torch.bfloat16) if with_delta else None
+    w = (1 + 0.1 * torch.randn(D, device=cuda)).bfloat16()
+    h, y, rstd = C.rmsnorm_fwd(x, d, w, 1e-5)
+    h_ref = x if d is None else x + d
+    y_ref = R.rmsnorm_ref(h_ref, w, 1e-5)
+    assert torch.equal(h, h_ref)
+    assert _rel(y, y_ref) < 1e-2
+    # exact same rounding points as the reference in >99% of elements
+    assert (y != y_ref).float().mean().item() < 0.01
+    dy = torch.randn_like(x)
+    dres = torch.randn_like(x) if with_delta else None
+    dw = torch.empty_like(w)
+    dx = C.rmsnorm_bwd(dy, h, w, rstd, dres, dw, False)
+    # fp32 autograd oracle
+    hf = h.float().requires_grad_()
+    wf = w.float().requires_grad_()
+    yf = (hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + 1e-5)) * wf
+    yf.backward(dy.float())
+    gx = hf.grad + (dres.float() if dres is not None else 0)
+    assert _rel(dx, gx) < 2e-2
+    assert _rel(dw, wf.grad) < 2e-2
+    # accumulate mode adds
+    dw2 = dw.clone()
+    C.rmsnorm_bwd(dy, h, w, rstd, dres, dw2, True)
+    assert _rel(dw2, 2 * dw.float()) < 1e-2
+
+
+def test_rope(cuda):
+    C = _ext.native()
+    B, S, Hq, Hkv, D = 2, 256, 4, 2, 128
+    fc = R.precompute_freqs_cis(D, S, 500000.0)
+    tab = R.rope_table(fc).to(cuda)
+    qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device=cuda, dtype=torch.bfloat16)
+    q = qkv[:, :Hq * D].view(B, S, Hq, D).clone()
+    k = qkv[:, Hq * D:(Hq + Hkv) * D].view(B, S, Hkv, D).clone()
+    v = qkv[:, (Hq + Hkv) * D:].clone()
+    qr, kr = R.apply_rotary_emb_ref(q, k, fc.to(cuda))
+    x = qkv.clone()
+    C.rope_(x, (Hq + Hkv) * D, tab, D, S, 0, False)
+    assert _rel(x[:, :Hq * D].view(B, S, Hq, D), qr) < 1e-2
+    assert _rel(x[:, Hq * D:(Hq + Hkv) * D].view(B, S, Hkv, D), kr) < 1e-2
+    assert torch.equal(x[:, (Hq + Hkv) * D:], v)
+    C.rope_(x, (Hq + Hkv) * D, tab, D, S, 0, True)  # inverse rotation restores
+    assert _rel(x, qkv) < 2e-2
+
+
+def test_swiglu(cuda):
+    C = _ext.native()
+    T, F = 300, 1024
+    gu = torch.randn(T, 2 * F, device=cuda, dtype=torch.bfloat16)
+    y = C.swiglu_fwd(gu)
+    y_ref = R.swiglu_ref(gu[:, :F], gu[:, F:])
+    assert _rel(y, y_ref) < 1e-2
+    dy = torch.randn(T, F, device=cuda, dtype=torch.bfloat16)
+    g = gu[:, :F].float().requires_grad_()
+    u = gu[:, F:].float().requires_grad_()
+    (torch.nn.functional.silu(g) * u).backward(dy.float())
+    dgu = C.swiglu_bwd(dy, gu, None)
+    assert _rel(dgu[:, :F], g.grad) < 2e-2
+    assert _rel(dgu[:, F:], u.grad) < 2e-2
+
+
+def test_embedding(cuda):
+    C = _ext.native()
+    V, D, T = 1000, 256, 4096
+    W = torch.randn(V, D, device=cuda, dtype=torch.bfloat16)
+    ids = torch.randint(0, V, (2, T // 2), device=cuda)
+    out = C.embedding_fwd(ids, W)
+    assert torch.equal(out, W[ids])
+    dout = torch.randn(2, T // 2, D, device=cuda, dtype=torch.bfloat16)
+    dW = torch.empty_like(W)
+    C.embedding_bwd(ids, dout, dW, False)
+    ref = torch.zeros(V, D, device=cuda).index_add_(0, ids.reshape(-1), dout.reshape(-1, D).float())
+    assert _rel(dW, ref) < 1e-2
+    dW2 = dW.clone()
+    C.embedding_bwd(ids, dout, dW2, False)
+    assert torch.equal(dW, dW2)  # deterministic
+
+
+@pytest.mark.parametrize("V", [32000, 50304, 1000])
+def test_cross_entropy(cuda, V):
+    C = _ext.native()
+    T = 257
+    logits = (3 * torch.randn(T, V, device=cuda)).bfloat16()
+    labels = torch.randint(0, V, (T,), device=cuda)
+    labels[:13] = -100
+    lse, loss_row, stats = C.xent_fwd(logits, labels, -100)
+    ref = R.cross_entropy_ref(logits, labels)
+    assert abs(stats[0].item() - ref.item()) < 1e-4 * max(1.0, ref.item())
+    assert stats[1].item() == (labels != -100).sum().item()
+    lf = logits.float().requires_grad_()
+    R.cross_entropy_ref(lf, labels).backward()
+    g = torch.full((1,), 0.5, device=cuda)
+    d = logits.clone()
+    C.xent_bwd_(d, labels, lse, stats, g, -100)
+    assert _rel(d, 0.5 * lf.grad) < 2e-2
+    assert d[:13].abs().max().item() == 0
+
+
+def test_adamw_matches_torch_fused(cuda):
+    C = _ext.native()
+    n = 1 << 20
+    torch.manual_seed(1)
+    p = torch.randn(n, device=cuda, dtype=torch.bfloat16)
+    g = torch.randn(n, device=cuda, dtype=torch.bfloat16)
+    m = torch.zeros_like(p)
+    v = torch.zeros_like(p)
+    p2, m2, v2 = p.clone(), m.clone(), v.clone()
+    step = torch.zeros((), device=cuda)
+    lr, b1, b2, eps, wd = 1e-3, 0.9, 0.999, 1e-8, 0.01
+    for s in range(1, 4):
+        C.adamw_flat_(p, g, m, v, lr, b1, b2, eps, wd, 1 - b1 ** s, math.sqrt(1 - b2 ** s), 1.0, None)
+        step += 1
+        torch._fused_adamw_([p2], [g], [m2], [v2], [], [step], amsgrad=False, lr=lr, beta1=b1, beta2=b2,
+                            weight_decay=wd, eps=eps, maximize=False)
+    assert (p != p2).float().mean().item() < 1e-3
+    assert _rel(p, p2) < 1e-2 and _rel(m, m2) < 1e-2 and _rel(v, v2) < 1e-2
+
+
+def test_grad_norm(cuda):
+    C = _ext.native()
+    x = torch.randn(3_000_001, device=cuda, dtype=torch.bfloat16)
+    out = C.grad_norm(x, 1.0, 1.0)
+    ref = x.float().norm()
+    assert abs(out[0].item() - ref.item()) < 1e-3 * ref.item()
+    assert abs(out[1].item() - min(1.0, 1.0 / (ref.item() + 1e-6))) < 1e-5
+
+
+# ------------------------------------------------------------------------------------------
+def _qkv(cuda, B, S, Hq, Hkv, D, seed=0, scale=1.0):
+    torch.manual_seed(seed)
+    qkv = (scale * torch.randn(B * S, (Hq + 2 * Hkv) * D, device=cuda)).bfloat16()
+    q = qkv[:, :Hq * D].view(B, S, Hq, D)
+    k = qkv[:, Hq * D:(Hq + Hkv) * D].view(B, S, Hkv, D)
+    v = qkv[:, (Hq + Hkv) * D:].view(B, S, Hkv, D)
+    return qkv, q, k, v
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv,D", [(1, 256, 4, 4, 128), (2, 512, 8, 2, 128), (1, 384, 4, 1, 64),
+                                          (1, 128, 2, 2, 64), (1, 192, 4, 2, 128)])
+@pytest.mark.parametrize("causal", [True, False])
+def test_attention_fwd(cuda, B, S, Hq, Hkv, D, causal):
+    C = _ext.native()
+    _, q, k, v = _qkv(cuda, B, S, Hq, Hkv, D)
+    scale = 1 / math.sqrt(D)
+    o, lse = C.attn_fwd(q, k, v, scale, causal)
+    o_ref, lse_ref = R.attention_lse_ref(q, k, v, causal, scale)
+    assert (o.float() - o_ref).abs().max().item() < 2e-2
+    assert (lse - lse_ref).abs().max().item() < 1e-3
+
+
+def test_attention_fwd_rescale_spike(cuda):
+    """Forces the online-softmax running max to jump at a late key tile (rule 26)."""
+    C = _ext.native()
+    B, S, H, D = 1, 512, 2, 128
+    _, q, k, v = _qkv(cuda, B, S, H, H, D, seed=3)
+    k = k.clone()
+    q = q.clone()
+    q[0, 400, 0] = 4.0
+    k[0, 390, 0] = 4.0  # huge score for query 400 at key tile 6
+    o, lse = C.attn_fwd(q, k, v, 1 / math.sqrt(D), True)
+    o_ref, lse_ref = R.attention_lse_ref(q, k, v, True, 1 / math.sqrt(D))
+    assert (o.float() - o_ref).abs().max().item() < 2e-2
+    assert (lse - lse_ref).abs().max().item() < 1e-3
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv,D", [(1, 256, 4, 4, 128), (2, 256, 8, 2, 128), (1, 384, 4, 1, 64),
+                                          (1, 128, 2, 2, 64)])
+@pytest.mark.parametrize("causal", [True, False])
+def test_attention_bwd(cuda, B, S, Hq, Hkv, D, causal):
+    C = _ext.native()
+    qkv, q, k, v = _qkv(cuda, B, S, Hq, Hkv, D, seed=1)
+    scale = 1 / math.sqrt(D)
+    o, lse = C.attn_fwd(q, k, v, scale, causal)
+    do = torch.randn(B, S, Hq, D, device=cuda).bfloat16()
+    dqkv = torch.zeros_like(qkv)
+    nq, nk = Hq * D, Hkv * D
+    dq = dqkv[:, :nq].view(B, S, Hq, D)
+    dk = dqkv[:, nq:nq + nk].view(B, S, Hkv, D)
+    dv = dqkv[:, nq + nk:].view(B, S, Hkv, D)
+    C.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, causal)
+    qf, kf, vf = (t.float().requires_grad_() for t in (q, k, v))
+    of, _ = R.attention_lse_ref(qf, kf, vf, causal, scale)
+    of.backward(do.float())
+    for got, want in ((dq, qf.grad), (dk, kf.grad), (dv, vf.grad)):
+        assert _rel(got, want) < 3e-2, (_rel(got, want))
+    # deterministic: identical bits on a second run
+    dqkv2 = torch.zeros_like(qkv)
+    C.attn_bwd(q, k, v, o, do, lse, dqkv2[:, :nq].view(B, S, Hq, D), dqkv2[:, nq:nq + nk].view(B, S, Hkv, D),
+               dqkv2[:, nq + nk:].view(B, S, Hkv, D), scale, causal)
+    assert torch.equal(dqkv, dqkv2)
+
+
+def test_single_hip_runtime_loaded(cuda):
+    """The extension must bind to torch's HIP runtime, not load a second copy."""
+    maps = open("/proc/self/maps").read()
+    libs = {line.split()[-1] for line in maps.splitlines() if "libamdhip64" in line}
+    assert len(libs) == 1, libs
