@@ -5,7 +5,7 @@
 // HIP stream of the tensor's device.
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <c10/core/DeviceGuard.h>
 
 #include "kernels/launchers.h"
 
@@ -32,6 +32,13 @@ void check_dev(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), "pyrecover_amd: ", name, " must be a GPU tensor");
 }
 
+// Every pointer handed to a kernel must live on the launch device (a host or foreign-device
+// pointer in a kernel argument is a GPU memory fault, not an exception).
+void same_dev(const at::Tensor& ref, const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.defined() && t.is_cuda() && t.device() == ref.device(), "pyrecover_amd: ", name,
+              " must be on ", ref.device(), " (got ", t.defined() ? t.device().str() : std::string("undefined"), ")");
+}
+
 void check_row_major(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1, "pyrecover_amd: ", name, " must be 2-D with unit inner stride");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "pyrecover_amd: ", name, " must be 16-B aligned");
@@ -45,8 +52,10 @@ std::vector<at::Tensor> rmsnorm_fwd(const at::Tensor& x, const c10::optional<at:
   const int64_t D = x.size(-1);
   const int64_t rows = x.numel() / D;
   TORCH_CHECK(w.numel() == D && w.scalar_type() == x.scalar_type(), "rmsnorm_fwd: weight mismatch");
+  same_dev(x, w, "rmsnorm weight");
+  if (delta.has_value()) same_dev(x, *delta, "rmsnorm delta");
   TORCH_CHECK(D % 8 == 0 && D <= 8192, "rmsnorm_fwd: D must be a multiple of 8 and <= 8192");
-  const c10::hip::HIPGuard guard(x.device());
+  const c10::DeviceGuard guard(x.device());
   at::Tensor y = at::empty_like(x);
   at::Tensor rstd = at::empty({rows}, x.options().dtype(at::kFloat));
   at::Tensor h;
@@ -72,7 +81,13 @@ at::Tensor rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at::Tens
   TORCH_CHECK(w.numel() == D && dw.numel() == D && dw.is_contiguous() && rstd.numel() == rows,
               "rmsnorm_bwd: shape mismatch");
   TORCH_CHECK(dw.scalar_type() == h.scalar_type() && dy.scalar_type() == h.scalar_type(), "rmsnorm_bwd: dtype");
-  const c10::hip::HIPGuard guard(h.device());
+  TORCH_CHECK(rstd.scalar_type() == at::kFloat && rstd.is_contiguous(), "rmsnorm_bwd: rstd must be contiguous fp32");
+  same_dev(dy, h, "h");
+  same_dev(dy, w, "w");
+  same_dev(dy, rstd, "rstd");
+  same_dev(dy, dw, "dw");
+  if (dres.has_value()) same_dev(dy, *dres, "dres");
+  const c10::DeviceGuard guard(h.device());
   at::Tensor dx = at::empty_like(h);
   const void* dr = nullptr;
   if (dres.has_value()) {
@@ -94,10 +109,11 @@ void rope_(at::Tensor x2d, int64_t ncols, const at::Tensor& tab, int64_t head_di
   check_dev(x2d, "x");
   check_row_major(x2d, "rope x");
   TORCH_CHECK(tab.scalar_type() == at::kFloat && tab.is_contiguous(), "rope: table must be contiguous fp32");
+  same_dev(x2d, tab, "rope table");
   TORCH_CHECK(tab.numel() >= (seq_len + pos_offset) * head_dim, "rope: table too small");
   TORCH_CHECK(ncols <= x2d.size(1) && ncols % head_dim == 0 && head_dim % 8 == 0, "rope: bad ncols/head_dim");
   TORCH_CHECK(x2d.size(0) % seq_len == 0, "rope: tokens must be a multiple of seq_len");
-  const c10::hip::HIPGuard guard(x2d.device());
+  const c10::DeviceGuard guard(x2d.device());
   check(pra_rope(dt(x2d), x2d.data_ptr(), tab.data_ptr(), x2d.size(0), (int)x2d.stride(0), (int)ncols, (int)head_dim,
                  (int)seq_len, (int)pos_offset, inverse ? 1 : 0, stream_of(x2d)),
         "rope");
@@ -109,7 +125,7 @@ at::Tensor swiglu_fwd(const at::Tensor& gu) {
   check_row_major(gu, "gu");
   TORCH_CHECK(gu.size(1) % 16 == 0, "swiglu: 2F must be a multiple of 16");
   const int64_t F = gu.size(1) / 2;
-  const c10::hip::HIPGuard guard(gu.device());
+  const c10::DeviceGuard guard(gu.device());
   at::Tensor y = at::empty({gu.size(0), F}, gu.options());
   const char* base = (const char*)gu.data_ptr();
   check(pra_swiglu_fwd(dt(gu), base, base + F * gu.element_size(), y.data_ptr(), gu.size(0), (int)F,
@@ -125,7 +141,9 @@ at::Tensor swiglu_bwd(const at::Tensor& dy, const at::Tensor& gu, c10::optional<
   check_row_major(dy, "dy");
   const int64_t F = gu.size(1) / 2;
   TORCH_CHECK(dy.size(0) == gu.size(0) && dy.size(1) == F && dy.scalar_type() == gu.scalar_type(), "swiglu_bwd: dy");
-  const c10::hip::HIPGuard guard(gu.device());
+  same_dev(gu, dy, "dy");
+  if (out.has_value()) same_dev(gu, *out, "out");
+  const c10::DeviceGuard guard(gu.device());
   at::Tensor dgu = out.has_value() ? *out : at::empty_like(gu);
   TORCH_CHECK(dgu.sizes() == gu.sizes() && dgu.strides() == gu.strides(), "swiglu_bwd: out layout");
   const char* g = (const char*)gu.data_ptr();
@@ -142,7 +160,7 @@ at::Tensor embedding_fwd(const at::Tensor& ids, const at::Tensor& W) {
   TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous() && ids.device() == W.device(),
               "embedding: ids must be contiguous int64 on the weight's device");
   TORCH_CHECK(W.dim() == 2 && W.is_contiguous() && W.size(1) % 8 == 0, "embedding: bad weight");
-  const c10::hip::HIPGuard guard(W.device());
+  const c10::DeviceGuard guard(W.device());
   auto sizes = ids.sizes().vec();
   sizes.push_back(W.size(1));
   at::Tensor out = at::empty(sizes, W.options());
@@ -157,7 +175,10 @@ void embedding_bwd(const at::Tensor& ids, const at::Tensor& dout, at::Tensor dW,
   check_dev(dW, "dW");
   TORCH_CHECK(dW.is_contiguous() && dout.is_contiguous() && dout.size(-1) == dW.size(1), "embedding_bwd: shapes");
   TORCH_CHECK(dout.numel() / dW.size(1) == ids.numel(), "embedding_bwd: ids/dout mismatch");
-  const c10::hip::HIPGuard guard(dW.device());
+  TORCH_CHECK(ids.scalar_type() == at::kLong && dout.scalar_type() == dW.scalar_type(), "embedding_bwd: dtypes");
+  same_dev(dW, ids, "ids");
+  same_dev(dW, dout, "dout");
+  const c10::DeviceGuard guard(dW.device());
   auto flat = ids.reshape({-1});
   auto sorted = at::sort(flat, /*stable=*/true, /*dim=*/0, /*descending=*/false);
   at::Tensor sids = std::get<0>(sorted).contiguous();
@@ -174,7 +195,8 @@ std::vector<at::Tensor> xent_fwd(const at::Tensor& logits, const at::Tensor& lab
   check_row_major(logits, "logits");
   TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_contiguous() && labels.numel() == logits.size(0),
               "xent: labels must be contiguous int64 [T]");
-  const c10::hip::HIPGuard guard(logits.device());
+  same_dev(logits, labels, "labels");
+  const c10::DeviceGuard guard(logits.device());
   const int64_t T = logits.size(0);
   auto fo = logits.options().dtype(at::kFloat);
   at::Tensor lse = at::empty({T}, fo), loss_row = at::empty({T}, fo), stats = at::empty({2}, fo);
@@ -191,7 +213,15 @@ void xent_bwd_(at::Tensor logits, const at::Tensor& labels, const at::Tensor& ls
   check_row_major(logits, "logits");
   TORCH_CHECK(grad_out.scalar_type() == at::kFloat && grad_out.numel() == 1 && grad_out.is_cuda(),
               "xent_bwd: grad_out must be a 1-element fp32 GPU tensor");
-  const c10::hip::HIPGuard guard(logits.device());
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_contiguous() && labels.numel() == logits.size(0),
+              "xent_bwd: labels");
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.numel() == logits.size(0) && stats.numel() == 2 &&
+              stats.scalar_type() == at::kFloat, "xent_bwd: lse/stats");
+  same_dev(logits, labels, "labels");
+  same_dev(logits, lse, "lse");
+  same_dev(logits, stats, "stats");
+  same_dev(logits, grad_out, "grad_out");
+  const c10::DeviceGuard guard(logits.device());
   check(pra_xent_bwd(dt(logits), logits.data_ptr(), labels.data_ptr<int64_t>(), lse.data_ptr<float>(),
                      stats.data_ptr<float>(), grad_out.data_ptr<float>(), logits.size(0), logits.size(1),
                      logits.stride(0), ignore_index, stream_of(logits)),
@@ -205,10 +235,14 @@ void adamw_flat_(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, 
   TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous(), "adamw: contiguous");
   TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(), "adamw: sizes");
   TORCH_CHECK(g.scalar_type() == p.scalar_type() && m.scalar_type() == v.scalar_type(), "adamw: dtypes");
-  const c10::hip::HIPGuard guard(p.device());
+  same_dev(p, g, "grad");
+  same_dev(p, m, "exp_avg");
+  same_dev(p, v, "exp_avg_sq");
+  const c10::DeviceGuard guard(p.device());
   const float* gsd = nullptr;
   if (gscale_dev.has_value()) {
-    TORCH_CHECK(gscale_dev->scalar_type() == at::kFloat && gscale_dev->is_cuda(), "adamw: gscale_dev fp32 GPU");
+    TORCH_CHECK(gscale_dev->scalar_type() == at::kFloat && gscale_dev->numel() >= 1, "adamw: gscale_dev fp32");
+    same_dev(p, *gscale_dev, "gscale_dev");
     gsd = gscale_dev->data_ptr<float>();
   }
   check(pra_adamw_flat(dt(p), dt(m), p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), (float)lr,
@@ -221,7 +255,7 @@ void adamw_flat_(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, 
 at::Tensor grad_norm(const at::Tensor& x, double max_norm, double pre_scale) {
   check_dev(x, "x");
   TORCH_CHECK(x.is_contiguous(), "grad_norm: contiguous");
-  const c10::hip::HIPGuard guard(x.device());
+  const c10::DeviceGuard guard(x.device());
   auto fo = x.options().dtype(at::kFloat);
   at::Tensor ws = at::empty({pra_sumsq_partials()}, fo), out = at::empty({2}, fo);
   check(pra_grad_norm(dt(x), x.data_ptr(), x.numel(), ws.data_ptr<float>(), out.data_ptr<float>(), (float)max_norm,
@@ -247,10 +281,12 @@ std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const
   check_bshd(q, "q", B, S, Hq, D);
   check_bshd(k, "k", B, S, Hkv, D);
   check_bshd(v, "v", B, S, Hkv, D);
+  same_dev(q, k, "k");
+  same_dev(q, v, "v");
   TORCH_CHECK(S % 64 == 0, "attention: seq_len must be a multiple of 64");
   TORCH_CHECK(D == 64 || D == 128, "attention: head_dim must be 64 or 128");
   TORCH_CHECK(Hq % Hkv == 0, "attention: n_heads must be a multiple of n_kv_heads");
-  const c10::hip::HIPGuard guard(q.device());
+  const c10::DeviceGuard guard(q.device());
   at::Tensor o = at::empty({B, S, Hq, D}, q.options());
   at::Tensor lse = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
   check(pra_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), (int)B, (int)S,
@@ -277,7 +313,8 @@ void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, con
   TORCH_CHECK(S % 128 == 0, "attention backward: seq_len must be a multiple of 128");
   TORCH_CHECK(D == 64 || D == 128, "attention: head_dim must be 64 or 128");
   TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.numel() == B * Hq * S && lse.is_contiguous(), "attention: lse");
-  const c10::hip::HIPGuard guard(q.device());
+  for (const at::Tensor& t : {k, v, o, dout, lse, dq, dk, dv}) same_dev(q, t, "attention operand");
+  const c10::DeviceGuard guard(q.device());
   at::Tensor delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
   check(pra_attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
                      delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), (int)B, (int)S, (int)Hq,

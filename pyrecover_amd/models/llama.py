@@ -86,7 +86,8 @@ class Transformer(nn.Module):
         self.vocab_size = model_args.vocab_size
         self.n_layers = model_args.n_layers
         self.tok_embeddings = nn.Embedding(model_args.vocab_size, model_args.dim)
-        self.register_buffer("freqs_cis", self._precompute_freqs_cis(), persistent=False)
+        dev = self.tok_embeddings.weight.device  # honour a `with torch.device(...)` construction
+        self.register_buffer("freqs_cis", self._precompute_freqs_cis().to(dev), persistent=False)
         self.layers = nn.ModuleDict()
         for layer_id in range(model_args.n_layers):
             self.layers[str(layer_id)] = TransformerBlock(layer_id, model_args)
@@ -103,9 +104,12 @@ class Transformer(nn.Module):
 
     def _apply(self, fn, recurse=True):
         out = super()._apply(fn, recurse)
-        # the rotation table always stays fp32 (it is a non-persistent buffer)
-        if self.rope_tab.dtype != torch.float32:
-            self.rope_tab = rope_table(self.freqs_cis.to(self.rope_tab.device))
+        # dtype casts must not touch the rotation tables: rebuild them (complex64 / fp32) on the
+        # buffers' (possibly new) device from the config, exactly as at construction.
+        dev = self.rope_tab.device
+        if self.freqs_cis.dtype != torch.complex64 or self.rope_tab.dtype != torch.float32:
+            self.freqs_cis = self._precompute_freqs_cis().to(dev)
+            self.rope_tab = rope_table(self.freqs_cis)
         if self.flat is not None and any(p.data.data_ptr() < self.flat.data.data_ptr() or
                                          p.data.data_ptr() >= self.flat.data.data_ptr() + self.flat.state_bytes()
                                          for p in self.parameters()):
