@@ -34,12 +34,18 @@ def parse():
     ap.add_argument("--lr", type=float, default=1e-5)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--profile-steps", type=int, default=0, help="emit roctx ranges for this many steps")
+    ap.add_argument("--gemm-tuning", choices=["auto", "off", "tune"], default="auto",
+                    help="hipBLASLt solution table (tuning/): auto = use the committed table if present")
     return ap.parse_args()
 
 
 def main():
     args = parse()
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    root = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, root)
+    from pyrecover_amd.utils.gemm_tuning import configure_gemm_tuning
+
+    configure_gemm_tuning(args.gemm_tuning)
     from pyrecover_amd.config import get_preset
     from pyrecover_amd.models.llama import Transformer
     from pyrecover_amd.optim.adamw import FlatAdamW
@@ -143,6 +149,10 @@ def main():
             "final_loss": round(final_loss, 4),
         }
         print(json.dumps(out), flush=True)
+    from pyrecover_amd.utils.gemm_tuning import flush_tuning
+
+    if rank == 0:
+        flush_tuning()
     if world > 1:
         torch.distributed.destroy_process_group()
 
