@@ -96,7 +96,7 @@ at::Tensor rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at::Tens
     dr = dres->data_ptr();
   }
   const int wsr = pra_rmsnorm_bwd_ws_rows((int)rows);
-  at::Tensor ws = at::empty({wsr, D}, h.options().dtype(at::kFloat));
+  at::Tensor ws = at::empty({wsr + 4, D}, h.options().dtype(at::kFloat));
   check(pra_rmsnorm_bwd(dt(h), dy.data_ptr(), h.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(), dr, dx.data_ptr(),
                         dw.data_ptr(), ws.data_ptr<float>(), (int)rows, (int)D, accumulate ? 1 : 0, stream_of(h)),
         "rmsnorm_bwd");

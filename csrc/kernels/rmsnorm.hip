@@ -129,14 +129,33 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
   }
 }
 
-// Deterministic column reduction of P partial rows: out[c] = (accumulate ? out[c] : 0) + sum_p part[p][c]
+// Deterministic two-stage column reduction of the P partial rows:
+//   stage 1: grid (ceil(D/64), 4): block (x, y) sums rows [y*ceil(P/4), ...) of 64 columns with
+//            4 waves interleaving rows, reduced through LDS in fixed order -> part2[y][D]
+//   stage 2: out[c] = (accumulate ? out[c] : 0) + part2[0][c] + ... + part2[3][c]
+__global__ __launch_bounds__(256) void colsum_stage1(const float* __restrict__ part, float* __restrict__ part2,
+                                                     int P, int D) {
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  const int per = (P + 3) / 4;
+  const int r0 = blockIdx.y * per, r1 = min(P, r0 + per);
+  float s = 0.f;
+  if (c < D)
+    for (int r = r0 + rg; r < r1; r += 4) s += part[(size_t)r * D + c];
+  red[rg][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rg == 0 && c < D)
+    part2[(size_t)blockIdx.y * D + c] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                                        red[3][threadIdx.x];
+}
+
 template <typename T>
-__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, T* __restrict__ out,
-                                                     int P, int D, int accumulate) {
+__global__ __launch_bounds__(256) void colsum_stage2(const float* __restrict__ part2, T* __restrict__ out, int D,
+                                                     int accumulate) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= D) return;
-  float s = 0.f;
-  for (int p = 0; p < P; ++p) s += part[(size_t)p * D + c];
+  float s = part2[c] + part2[D + c] + part2[2 * D + c] + part2[3 * D + c];
   if (accumulate) s += to_f<T>(out[c]);
   out[c] = from_f<T>(s);
 }
@@ -165,8 +184,9 @@ static hipError_t bwd_impl(const void* dy, const void* h, const void* w, const f
   else
     hipLaunchKernelGGL((rmsnorm_bwd_kernel<T, NVB, false>), dim3(blocks), dim3(256), 0, s, (const T*)dy,
                        (const T*)h, (const T*)w, rstd, (const T*)nullptr, (T*)dx, ws, rows, D);
-  hipLaunchKernelGGL((colsum_kernel<T>), dim3((D + 255) / 256), dim3(256), 0, s, ws, (T*)dw, ws_rows, D,
-                     accumulate);
+  float* part2 = ws + (size_t)ws_rows * D;
+  hipLaunchKernelGGL(colsum_stage1, dim3((D + 63) / 64, 4), dim3(256), 0, s, ws, part2, ws_rows, D);
+  hipLaunchKernelGGL((colsum_stage2<T>), dim3((D + 255) / 256), dim3(256), 0, s, part2, (T*)dw, D, accumulate);
   return hipGetLastError();
 }
 
@@ -190,7 +210,9 @@ static hipError_t bwd_impl(const void* dy, const void* h, const void* w, const f
 extern "C" {
 
 // Number of fp32 workspace rows (each D floats) the backward needs for `rows` rows.
-int pra_rmsnorm_bwd_ws_rows(int rows) { return rows < 512 ? rows : 512; }
+// Blocks of the backward kernel (= fp32 partial rows of dw); the workspace must hold
+// pra_rmsnorm_bwd_ws_rows(rows) + 4 rows of D floats.
+int pra_rmsnorm_bwd_ws_rows(int rows) { return rows < 256 ? rows : 256; }
 
 hipError_t pra_rmsnorm_fwd(int dtype, const void* x, const void* delta, const void* w, void* h_out,
                            void* y, float* rstd, int rows, int D, float eps, hipStream_t s) {

@@ -149,6 +149,14 @@ struct Record {
   uint64_t nbytes;
 };
 
+// One file = a sequence of items: a zip archive built from records, or raw bytes copied verbatim.
+struct Item {
+  bool raw = false;
+  uintptr_t ptr = 0;  // raw
+  uint64_t n = 0;     // raw
+  std::vector<Record> records;  // zip
+};
+
 struct Chunk {
   uintptr_t host;  // host address
   uint64_t n;
@@ -162,7 +170,28 @@ struct JobResult {
   uint64_t bytes = 0;
   double seconds = 0;
   double stage_wait_seconds = 0;
+  std::vector<std::pair<uint64_t, uint64_t>> items;  // (offset, length) of each item in the file
 };
+
+// Streaming MD5 of an open file from its start (double-buffered reads on this thread, hashing
+// on the Md5Pipe thread).
+std::string md5_fd(int fd) {
+  Md5Pipe md5;
+  constexpr size_t kBuf = 32u << 20;
+  uint64_t pos = 0;
+  for (;;) {
+    auto buf = std::make_shared<std::vector<uint8_t>>(kBuf);
+    ssize_t n;
+    do {
+      n = ::pread(fd, buf->data(), kBuf, (off_t)pos);
+    } while (n < 0 && errno == EINTR);
+    if (n < 0) throw std::runtime_error("md5: read failed");
+    if (n == 0) break;
+    md5.push_copy(buf->data(), (size_t)n);
+    pos += (uint64_t)n;
+  }
+  return md5.finish();
+}
 
 // ------------------------------------------------------------------------------------------
 class CkptEngine {
@@ -272,15 +301,15 @@ class CkptEngine {
 
   // Start writing a zip archive on the background thread. Records point into the pinned pool
   // (waited per chunk) or into caller-owned host memory kept alive until wait().
-  void write_zip(const std::string& path, std::vector<Record> records, bool want_md5, bool do_fsync) {
+  void write_items(const std::string& path, std::vector<Item> items, bool want_md5, bool do_fsync) {
     wait_writer();
     running_ = true;
     result_ = JobResult{};
-    writer_ = std::thread([this, path, records = std::move(records), want_md5, do_fsync]() mutable {
+    writer_ = std::thread([this, path, items = std::move(items), want_md5, do_fsync]() mutable {
       JobResult r;
       const auto t0 = std::chrono::steady_clock::now();
       try {
-        write_impl(path, records, want_md5, do_fsync, r);
+        write_impl(path, items, want_md5, do_fsync, r);
         r.ok = true;
       } catch (const std::exception& e) {
         r.ok = false;
@@ -313,6 +342,9 @@ class CkptEngine {
     d["bytes"] = result_.bytes;
     d["seconds"] = result_.seconds;
     d["stage_wait_seconds"] = result_.stage_wait_seconds;
+    py::list items;
+    for (auto& it : result_.items) items.append(py::make_tuple(it.first, it.second));
+    d["items"] = items;
     return d;
   }
 
@@ -362,10 +394,131 @@ class CkptEngine {
     }
   }
 
-  void write_impl(const std::string& path, std::vector<Record>& recs, bool want_md5, bool do_fsync, JobResult& r) {
+  // Emit one zip archive (offsets inside it are relative to `base`, the archive's first byte).
+  template <class Emit>
+  void emit_zip(std::vector<Record>& recs, uint64_t& off, const uint64_t base, int fd, Md5Pipe* md5, Emit&& emit_copy,
+                JobResult& r) {
+    struct CdEnt {
+      std::string name;
+      uint32_t crc;
+      uint64_t size, hdr_off;
+    };
+    std::vector<CdEnt> cd;
+    for (auto& rec : recs) {
+      const uint64_t hdr_off = off - base;
+      const bool z64 = rec.nbytes >= 0xFFFFFFFFull;
+      std::vector<uint8_t> h;
+      put32(h, 0x04034b50);
+      put16(h, z64 ? 45 : 20);  // version needed
+      put16(h, 0x0800);         // UTF-8 names, no data descriptor
+      put16(h, 0);              // stored
+      put16(h, 0);
+      put16(h, 0x21);           // dos time/date (1980-01-01)
+      // CRC first (parallel pieces over the staged bytes), so every byte is final when written
+      // and the MD5 pipe can hash the stream as it goes.
+      wait_range(rec.ptr, rec.nbytes, r);
+      const uint32_t crc = crc32_parallel(0, (const uint8_t*)rec.ptr, rec.nbytes);
+      put32(h, crc);
+      put32(h, z64 ? 0xFFFFFFFFu : (uint32_t)rec.nbytes);
+      put32(h, z64 ? 0xFFFFFFFFu : (uint32_t)rec.nbytes);
+      put16(h, (uint16_t)rec.name.size());
+      const size_t extra_len_pos = h.size();
+      put16(h, 0);
+      h.insert(h.end(), rec.name.begin(), rec.name.end());
+      std::vector<uint8_t> ex;
+      if (z64) {
+        put16(ex, 0x0001);
+        put16(ex, 16);
+        put64(ex, rec.nbytes);
+        put64(ex, rec.nbytes);
+      }
+      // 64-byte alignment (relative to the archive start) of the payload via a padding extra
+      // field ("FB", like torch's writer), so mmap'ed loads see aligned storages
+      const uint64_t data_start = hdr_off + h.size() + ex.size();
+      const uint64_t pad = (64 - (data_start + 4) % 64) % 64;
+      put16(ex, 0x4246);
+      put16(ex, (uint16_t)pad);
+      ex.insert(ex.end(), pad, 0);
+      h[extra_len_pos] = ex.size() & 0xff;
+      h[extra_len_pos + 1] = ex.size() >> 8;
+      h.insert(h.end(), ex.begin(), ex.end());
+      emit_copy(h);
+      constexpr uint64_t kPiece = 64ull << 20;
+      for (uint64_t o = 0; o < rec.nbytes; o += kPiece) {
+        const uint64_t n = std::min(kPiece, rec.nbytes - o);
+        const uint8_t* p = (const uint8_t*)(rec.ptr + o);
+        write_all(fd, p, n);
+        if (md5) md5->push_borrowed(p, n);
+        off += n;
+      }
+      cd.push_back({rec.name, crc, rec.nbytes, hdr_off});
+    }
+    const uint64_t cd_off = off - base;
+    std::vector<uint8_t> c;
+    for (auto& e : cd) {
+      const bool zs = e.size >= 0xFFFFFFFFull, zo = e.hdr_off >= 0xFFFFFFFFull;
+      std::vector<uint8_t> ex;
+      if (zs || zo) {
+        put16(ex, 0x0001);
+        put16(ex, (uint16_t)((zs ? 16 : 0) + (zo ? 8 : 0)));
+        if (zs) { put64(ex, e.size); put64(ex, e.size); }
+        if (zo) put64(ex, e.hdr_off);
+      }
+      put32(c, 0x02014b50);
+      put16(c, (3 << 8) | 45);  // made by: unix, 4.5
+      put16(c, (zs || zo) ? 45 : 20);
+      put16(c, 0x0800);
+      put16(c, 0);
+      put16(c, 0);
+      put16(c, 0x21);
+      put32(c, e.crc);
+      put32(c, zs ? 0xFFFFFFFFu : (uint32_t)e.size);
+      put32(c, zs ? 0xFFFFFFFFu : (uint32_t)e.size);
+      put16(c, (uint16_t)e.name.size());
+      put16(c, (uint16_t)ex.size());
+      put16(c, 0);  // comment
+      put16(c, 0);  // disk
+      put16(c, 0);  // internal attr
+      put32(c, 0100644u << 16);
+      put32(c, zo ? 0xFFFFFFFFu : (uint32_t)e.hdr_off);
+      c.insert(c.end(), e.name.begin(), e.name.end());
+      c.insert(c.end(), ex.begin(), ex.end());
+    }
+    const uint64_t cd_size = c.size();
+    const uint64_t n = cd.size();
+    const bool z64e = cd_off >= 0xFFFFFFFFull || cd_size >= 0xFFFFFFFFull || n >= 0xFFFF;
+    if (z64e) {
+      const uint64_t z64_off = cd_off + cd_size;
+      put32(c, 0x06064b50);
+      put64(c, 44);
+      put16(c, (3 << 8) | 45);
+      put16(c, 45);
+      put32(c, 0);
+      put32(c, 0);
+      put64(c, n);
+      put64(c, n);
+      put64(c, cd_size);
+      put64(c, cd_off);
+      put32(c, 0x07064b50);
+      put32(c, 0);
+      put64(c, z64_off);
+      put32(c, 1);
+    }
+    put32(c, 0x06054b50);
+    put16(c, 0);
+    put16(c, 0);
+    put16(c, z64e ? 0xFFFF : (uint16_t)n);
+    put16(c, z64e ? 0xFFFF : (uint16_t)n);
+    put32(c, z64e ? 0xFFFFFFFFu : (uint32_t)cd_size);
+    put32(c, z64e ? 0xFFFFFFFFu : (uint32_t)cd_off);
+    put16(c, 0);
+    emit_copy(c);
+  }
+
+  void write_impl(const std::string& path, std::vector<Item>& items, bool want_md5, bool do_fsync, JobResult& r) {
     if (device_ >= 0) hip_check(hipSetDevice(device_), "hipSetDevice");
     const std::string tmp = path + ".tmp";
-    const int fd = ::open(tmp.c_str(), O_CREAT | O_TRUNC | O_WRONLY | O_CLOEXEC, 0644);
+    const int fd = ::open(tmp.c_str(), O_CREAT | O_TRUNC | O_RDWR | O_CLOEXEC, 0644);
     if (fd < 0) throw std::runtime_error("ckpt_engine: cannot open " + tmp + ": " + strerror(errno));
     std::unique_ptr<Md5Pipe> md5;
     if (want_md5) md5 = std::make_unique<Md5Pipe>();
@@ -375,133 +528,28 @@ class CkptEngine {
       if (md5) md5->push_copy(b.data(), b.size());
       off += b.size();
     };
-    struct CdEnt {
-      std::string name;
-      uint32_t crc;
-      uint64_t size, hdr_off;
-    };
-    std::vector<CdEnt> cd;
     try {
-      for (auto& rec : recs) {
-        const uint64_t hdr_off = off;
-        const bool z64 = rec.nbytes >= 0xFFFFFFFFull;
-        std::vector<uint8_t> h;
-        put32(h, 0x04034b50);
-        put16(h, z64 ? 45 : 20);  // version needed
-        put16(h, 0x0800);         // UTF-8 names, no data descriptor
-        put16(h, 0);              // stored
-        put16(h, 0);
-        put16(h, 0x21);           // dos time/date (1980-01-01)
-        const size_t crc_pos = h.size();
-        put32(h, 0);              // crc (patched)
-        put32(h, z64 ? 0xFFFFFFFFu : (uint32_t)rec.nbytes);
-        put32(h, z64 ? 0xFFFFFFFFu : (uint32_t)rec.nbytes);
-        put16(h, (uint16_t)rec.name.size());
-        const size_t extra_len_pos = h.size();
-        put16(h, 0);
-        h.insert(h.end(), rec.name.begin(), rec.name.end());
-        std::vector<uint8_t> ex;
-        if (z64) {
-          put16(ex, 0x0001);
-          put16(ex, 16);
-          put64(ex, rec.nbytes);
-          put64(ex, rec.nbytes);
+      for (auto& it : items) {
+        const uint64_t start = off;
+        if (it.raw) {
+          wait_range(it.ptr, it.n, r);
+          write_all(fd, (const void*)it.ptr, it.n);
+          if (md5) md5->push_borrowed((const void*)it.ptr, it.n);
+          off += it.n;
+        } else {
+          emit_zip(it.records, off, start, fd, md5.get(), emit_copy, r);
         }
-        // 64-byte alignment of the payload via a padding extra field ("FB", like torch)
-        uint64_t data_start = hdr_off + h.size() + ex.size();
-        uint64_t pad = (64 - (data_start + 4) % 64) % 64;
-        put16(ex, 0x4246);
-        put16(ex, (uint16_t)pad);
-        ex.insert(ex.end(), pad, 0);
-        h[extra_len_pos] = ex.size() & 0xff;
-        h[extra_len_pos + 1] = ex.size() >> 8;
-        h.insert(h.end(), ex.begin(), ex.end());
-        emit_copy(h);
-        // payload, in pieces, waiting for the staging chunks it covers
-        uint32_t crc = 0;
-        constexpr uint64_t kPiece = 64ull << 20;
-        for (uint64_t o = 0; o < rec.nbytes; o += kPiece) {
-          const uint64_t n = std::min(kPiece, rec.nbytes - o);
-          const uint8_t* p = (const uint8_t*)(rec.ptr + o);
-          wait_range((uintptr_t)p, n, r);
-          crc = crc32_parallel(crc, p, n);
-          write_all(fd, p, n);
-          if (md5) md5->push_borrowed(p, n);
-          off += n;
-        }
-        uint8_t cb[4] = {(uint8_t)crc, (uint8_t)(crc >> 8), (uint8_t)(crc >> 16), (uint8_t)(crc >> 24)};
-        if (::pwrite(fd, cb, 4, (off_t)(hdr_off + crc_pos)) != 4) throw std::runtime_error("ckpt_engine: pwrite crc");
-        cd.push_back({rec.name, crc, rec.nbytes, hdr_off});
+        r.items.push_back({start, off - start});
       }
-      // central directory
-      const uint64_t cd_off = off;
-      std::vector<uint8_t> c;
-      for (auto& e : cd) {
-        const bool zs = e.size >= 0xFFFFFFFFull, zo = e.hdr_off >= 0xFFFFFFFFull;
-        std::vector<uint8_t> ex;
-        if (zs || zo) {
-          put16(ex, 0x0001);
-          put16(ex, (uint16_t)((zs ? 16 : 0) + (zo ? 8 : 0)));
-          if (zs) { put64(ex, e.size); put64(ex, e.size); }
-          if (zo) put64(ex, e.hdr_off);
-        }
-        put32(c, 0x02014b50);
-        put16(c, (3 << 8) | 45);  // made by: unix, 4.5
-        put16(c, (zs || zo) ? 45 : 20);
-        put16(c, 0x0800);
-        put16(c, 0);
-        put16(c, 0);
-        put16(c, 0x21);
-        put32(c, e.crc);
-        put32(c, zs ? 0xFFFFFFFFu : (uint32_t)e.size);
-        put32(c, zs ? 0xFFFFFFFFu : (uint32_t)e.size);
-        put16(c, (uint16_t)e.name.size());
-        put16(c, (uint16_t)ex.size());
-        put16(c, 0);  // comment
-        put16(c, 0);  // disk
-        put16(c, 0);  // internal attr
-        put32(c, 0100644u << 16);
-        put32(c, zo ? 0xFFFFFFFFu : (uint32_t)e.hdr_off);
-        c.insert(c.end(), e.name.begin(), e.name.end());
-        c.insert(c.end(), ex.begin(), ex.end());
-      }
-      const uint64_t cd_size = c.size();
-      const uint64_t n = cd.size();
-      const bool z64e = cd_off >= 0xFFFFFFFFull || cd_size >= 0xFFFFFFFFull || n >= 0xFFFF;
-      if (z64e) {
-        const uint64_t z64_off = cd_off + cd_size;
-        put32(c, 0x06064b50);
-        put64(c, 44);
-        put16(c, (3 << 8) | 45);
-        put16(c, 45);
-        put32(c, 0);
-        put32(c, 0);
-        put64(c, n);
-        put64(c, n);
-        put64(c, cd_size);
-        put64(c, cd_off);
-        put32(c, 0x07064b50);
-        put32(c, 0);
-        put64(c, z64_off);
-        put32(c, 1);
-      }
-      put32(c, 0x06054b50);
-      put16(c, 0);
-      put16(c, 0);
-      put16(c, z64e ? 0xFFFF : (uint16_t)n);
-      put16(c, z64e ? 0xFFFF : (uint16_t)n);
-      put32(c, z64e ? 0xFFFFFFFFu : (uint32_t)cd_size);
-      put32(c, z64e ? 0xFFFFFFFFu : (uint32_t)cd_off);
-      put16(c, 0);
-      emit_copy(c);
       if (do_fsync && ::fsync(fd) != 0) throw std::runtime_error("ckpt_engine: fsync failed");
+      // Whole-file MD5 (the reference's `.md5` sidecar: 32 hex chars, no newline).
+      if (md5) r.md5 = md5->finish();
     } catch (...) {
       ::close(fd);
       if (md5) md5->finish();
       throw;
     }
     ::close(fd);
-    if (md5) r.md5 = md5->finish();
     r.bytes = off;
     if (::rename(tmp.c_str(), path.c_str()) != 0)
       throw std::runtime_error("ckpt_engine: rename failed: " + std::string(strerror(errno)));
@@ -535,22 +583,15 @@ std::string md5_file(const std::string& path) {
   py::gil_scoped_release nogil;
   const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
   if (fd < 0) throw std::runtime_error("md5_file: cannot open " + path);
-  Md5Pipe md5;
-  constexpr size_t kBuf = 32u << 20;
-  std::vector<std::shared_ptr<std::vector<uint8_t>>> ring;
-  for (;;) {
-    auto buf = std::make_shared<std::vector<uint8_t>>(kBuf);
-    const ssize_t n = ::read(fd, buf->data(), kBuf);
-    if (n < 0) {
-      if (errno == EINTR) continue;
-      ::close(fd);
-      throw std::runtime_error("md5_file: read failed");
-    }
-    if (n == 0) break;
-    md5.push_copy(buf->data(), (size_t)n);
+  std::string h;
+  try {
+    h = md5_fd(fd);
+  } catch (...) {
+    ::close(fd);
+    throw;
   }
   ::close(fd);
-  return md5.finish();
+  return h;
 }
 
 uint32_t crc32_bytes(py::bytes b) {
@@ -569,12 +610,29 @@ void register_ckpt_engine(py::module& m) {
       .def("stage", &CkptEngine::stage)
       .def("fence", &CkptEngine::fence)
       .def("sync_stage", &CkptEngine::sync_stage)
-      .def("write_zip",
-           [](CkptEngine& e, const std::string& path, const std::vector<std::tuple<std::string, uintptr_t, uint64_t>>& recs,
-              bool md5, bool fsync) {
-             std::vector<Record> r;
-             for (auto& t : recs) r.push_back({std::get<0>(t), std::get<1>(t), std::get<2>(t)});
-             e.write_zip(path, std::move(r), md5, fsync);
+      .def("write_items",
+           [](CkptEngine& e, const std::string& path, py::list items, bool md5, bool fsync) {
+             // items: [("raw", ptr, nbytes) | ("zip", [(name, ptr, nbytes), ...])]
+             std::vector<Item> v;
+             for (auto h : items) {
+               auto t = h.cast<py::tuple>();
+               Item it;
+               const std::string kind = t[0].cast<std::string>();
+               if (kind == "raw") {
+                 it.raw = true;
+                 it.ptr = t[1].cast<uintptr_t>();
+                 it.n = t[2].cast<uint64_t>();
+               } else if (kind == "zip") {
+                 for (auto rh : t[1].cast<py::list>()) {
+                   auto rt = rh.cast<py::tuple>();
+                   it.records.push_back({rt[0].cast<std::string>(), rt[1].cast<uintptr_t>(), rt[2].cast<uint64_t>()});
+                 }
+               } else {
+                 throw std::runtime_error("write_items: unknown item kind " + kind);
+               }
+               v.push_back(std::move(it));
+             }
+             e.write_items(path, std::move(v), md5, fsync);
            })
       .def("busy", &CkptEngine::busy)
       .def("wait", &CkptEngine::wait);

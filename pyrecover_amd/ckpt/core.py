@@ -1,0 +1,300 @@
+"""Checkpoint engine front-end: state collection, staging, async jobs, latest/retention.
+
+Everything here is format-agnostic; :mod:`.vanilla` and :mod:`.sharded` build on it.
+
+Staging: all tensors of a checkpoint state are mapped to contiguous byte regions of their
+storages (the flat parameter / Adam buffers collapse into a few large regions), copied by the
+C++ engine into a reusable pinned host pool (device: hipMemcpyAsync on a low-priority stream;
+CPU: parallel memcpy) and replaced in the state by CPU tensors aliasing the pool. The archive
+writer thread then streams them to disk while training continues; :meth:`Checkpointer.fence`
+makes the compute stream wait for the snapshot before the optimizer mutates parameters again.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import random
+import re
+import shutil
+import threading
+import time
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Any, Callable, Dict, List, Optional, Tuple
+
+import torch
+
+from .. import _ext
+from .serialization import host_view
+
+logger = logging.getLogger("pyrecover")
+
+_MERGE_GAP = 4096  # bytes: merge staging regions separated by small alignment gaps
+
+
+# ------------------------------------------------------------------------------------------
+def unwrap(model):
+    m = model
+    while True:
+        if hasattr(m, "module") and isinstance(getattr(m, "module"), torch.nn.Module):
+            m = m.module
+        elif hasattr(m, "_orig_mod") and isinstance(getattr(m, "_orig_mod"), torch.nn.Module):
+            m = m._orig_mod
+        else:
+            return m
+
+
+_PREFIX_RE = re.compile(r"^(module\.|_orig_mod\.)+")
+
+
+def strip_prefixes(sd: Dict[str, Any]) -> Dict[str, Any]:
+    """World-size / compile agnostic keys."""
+    return {_PREFIX_RE.sub("", k): v for k, v in sd.items()}
+
+
+def capture_rng_state() -> Dict[str, Any]:
+    st = {"torch_cpu": torch.get_rng_state(), "python": random.getstate()}
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        st["torch_cuda"] = torch.cuda.get_rng_state_all()
+    return st
+
+
+def restore_rng_state(st: Dict[str, Any]):
+    if not st:
+        return
+    if "torch_cpu" in st:
+        torch.set_rng_state(st["torch_cpu"])
+    if "python" in st:
+        v = st["python"]
+        random.setstate((v[0], tuple(v[1]), v[2]))
+    if "torch_cuda" in st and torch.cuda.is_available():
+        states = st["torch_cuda"]
+        if len(states) == torch.cuda.device_count():
+            torch.cuda.set_rng_state_all(states)
+
+
+def build_state(model, optimizer, lr_scheduler=None, sampler=None, step: int = 0, epoch: Optional[int] = None,
+                extra: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
+    """The reference's vanilla checkpoint dict (reference pyrecover/checkpoint.py:60-73) plus a
+    ``pyrecover_state`` entry (RNG, sampler cursor, run metadata) that reference loaders ignore."""
+    m = unwrap(model)
+    state: Dict[str, Any] = {
+        "epoch": epoch,
+        "step": step,
+        "model": strip_prefixes(m.state_dict()),
+        "optimizer": optimizer.state_dict(),
+    }
+    if lr_scheduler is not None:
+        state["lr_scheduler"] = lr_scheduler.state_dict()
+    if sampler is not None and hasattr(sampler, "set_state"):
+        state["sampler_state"] = sampler.state_dict()
+    ps = {"format": "pyrecover_amd/1", "rng": capture_rng_state(), "saved_at": time.time()}
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        ps["world_size"] = torch.distributed.get_world_size()
+    if extra:
+        ps.update(extra)
+    state["pyrecover_state"] = ps
+    return state
+
+
+# ------------------------------------------------------------------------------------------
+def _walk(obj, fn):
+    """Rebuild a nested dict/list/tuple structure with fn applied to tensor leaves."""
+    if isinstance(obj, torch.Tensor):
+        return fn(obj)
+    if isinstance(obj, dict):
+        return obj.__class__((k, _walk(v, fn)) for k, v in obj.items())
+    if isinstance(obj, list):
+        return [_walk(v, fn) for v in obj]
+    if isinstance(obj, tuple):
+        return tuple(_walk(v, fn) for v in obj)
+    return obj
+
+
+def _tensors(obj, out: List[torch.Tensor]):
+    if isinstance(obj, torch.Tensor):
+        out.append(obj)
+    elif isinstance(obj, dict):
+        for v in obj.values():
+            _tensors(v, out)
+    elif isinstance(obj, (list, tuple)):
+        for v in obj:
+            _tensors(v, out)
+    return out
+
+
+class Checkpointer:
+    """Per-device staging pool + background writer (one in-flight archive per device)."""
+
+    _instances: Dict[int, "Checkpointer"] = {}
+
+    @classmethod
+    def get(cls, device: torch.device) -> "Checkpointer":
+        idx = device.index if device.type == "cuda" else -1
+        if device.type == "cuda" and idx is None:
+            idx = torch.cuda.current_device()
+        if idx not in cls._instances:
+            cls._instances[idx] = Checkpointer(idx)
+        return cls._instances[idx]
+
+    def __init__(self, device_index: int):
+        self.device_index = device_index
+        self.engine = _ext.native().CkptEngine(device_index)
+        self.pending: Optional["Job"] = None
+        self.staged = False
+
+    # -- staging -------------------------------------------------------------------------
+    def stage(self, obj):
+        """Snapshot every tensor of ``obj`` on this checkpointer's device into the pinned pool;
+        return ``obj`` rebuilt with CPU tensors aliasing the pool (other tensors are cloned)."""
+        self.wait()  # pool reuse: the previous archive must be on disk
+        dev_is_cuda = self.device_index >= 0
+        ts = _tensors(obj, [])
+        spans: List[Tuple[int, int, int]] = []  # (ptr, nbytes, storage base)
+        for t in ts:
+            on_dev = t.is_cuda if dev_is_cuda else (not t.is_cuda)
+            if not on_dev or t.numel() == 0:
+                continue
+            if not t.is_contiguous():
+                raise ValueError("checkpoint tensors must be contiguous")
+            spans.append((t.data_ptr(), t.numel() * t.element_size(), t.untyped_storage().data_ptr()))
+        spans.sort()
+        regions: List[List[int]] = []  # [ptr, nbytes, storage base]
+        for p, n, sb in spans:
+            # merge only inside ONE storage: a gap between two allocations may be unmapped memory
+            if regions and regions[-1][2] == sb and p <= regions[-1][0] + regions[-1][1] + _MERGE_GAP:
+                regions[-1][1] = max(regions[-1][1], p + n - regions[-1][0])
+            else:
+                regions.append([p, n, sb])
+        total = sum(r[1] for r in regions) + 64 * len(regions)
+        if total > self.engine.pool_size():
+            self.engine.reserve(int(total * 1.05) + (1 << 20))
+        offs = self.engine.stage([(r[0], r[1]) for r in regions]) if regions else []
+        base = self.engine.pool_ptr()
+        starts = [r[0] for r in regions]
+        import bisect
+
+        def to_host(t: torch.Tensor):
+            on_dev = t.is_cuda if dev_is_cuda else (not t.is_cuda)
+            if not on_dev or t.numel() == 0:
+                return t.detach().to("cpu", copy=True)
+            i = bisect.bisect_right(starts, t.data_ptr()) - 1
+            host = base + offs[i] + (t.data_ptr() - starts[i])
+            return host_view(host, t.numel() * t.element_size(), t.dtype, tuple(t.shape))
+
+        self.staged = True
+        return _walk(obj, to_host)
+
+    def fence(self):
+        """Make the current compute stream wait (GPU-side) for the in-flight snapshot."""
+        if self.staged and self.device_index >= 0:
+            self.engine.fence()
+
+    def sync_stage(self):
+        if self.staged:
+            self.engine.sync_stage()
+
+    # -- writing -------------------------------------------------------------------------
+    def write(self, path: str, items, md5: bool, fsync: bool, keepalive, on_done: Optional[Callable] = None) -> "Job":
+        self.wait()
+        os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
+        self.engine.write_items(str(path), items, md5, fsync)
+        self.pending = Job(self, str(path), keepalive, on_done)
+        return self.pending
+
+    def busy(self) -> bool:
+        return self.engine.busy()
+
+    def wait(self) -> Optional[Dict[str, Any]]:
+        job, self.pending = self.pending, None
+        if job is None:
+            return None
+        return job.wait()
+
+
+@dataclass
+class Job:
+    ckpt: Checkpointer
+    path: str
+    keepalive: Any
+    on_done: Optional[Callable]
+    result: Optional[Dict[str, Any]] = None
+
+    def wait(self) -> Dict[str, Any]:
+        if self.result is None:
+            self.result = self.ckpt.engine.wait()
+            self.keepalive = None
+            if not self.result["ok"]:
+                raise RuntimeError(f"checkpoint write to {self.path} failed: {self.result['error']}")
+            if self.on_done is not None:
+                self.on_done(self.result)
+        return self.result
+
+
+def wait_all():
+    """Drain every in-flight checkpoint write on this process."""
+    out = []
+    for c in Checkpointer._instances.values():
+        r = c.wait()
+        if r is not None:
+            out.append(r)
+    return out
+
+
+def fence_all():
+    for c in Checkpointer._instances.values():
+        c.fence()
+
+
+# ------------------------------------------------------------------------------------------
+_STEP_RE = re.compile(r"ckpt_(\d+)(_final)?")
+
+
+def ckpt_step(p: Path) -> Tuple[int, int]:
+    m = _STEP_RE.search(p.name)
+    if not m:
+        return (-1, 0)
+    return (int(m.group(1)), 1 if m.group(2) else 0)
+
+
+def is_complete_dir(d: Path) -> bool:
+    return (d / ".metadata").exists() and not (d / ".incomplete").exists()
+
+
+def get_latest_checkpoint(checkpoint_dir: str, distributed: bool = False) -> Optional[str]:
+    """Newest checkpoint by mtime, like reference pyrecover/checkpoint.py:371-404; sharded
+    directories count only once complete (``.metadata`` written, no ``.incomplete`` marker)."""
+    base = Path(checkpoint_dir)
+    if not base.exists():
+        return None
+    if distributed:
+        items = [x for x in base.glob("ckpt_*") if x.is_dir() and is_complete_dir(x)]
+    else:
+        items = [x for x in base.glob("**/*.pt") if x.is_file()]
+    if not items:
+        return None
+    items.sort(key=lambda x: (x.stat().st_mtime, ckpt_step(x)))
+    return str(items[-1])
+
+
+def apply_retention(base: Path, max_keep: int, distributed: bool):
+    """Keep the newest ``max_keep`` checkpoints by step number (fixes the reference's
+    lexicographic sort); only ``ckpt_*`` entries are ever deleted."""
+    if max_keep <= 0:
+        return
+    if distributed:
+        items = [d for d in base.glob("ckpt_*") if d.is_dir() and is_complete_dir(d)]
+    else:
+        items = [f for f in base.glob("**/*.pt") if f.is_file() and _STEP_RE.search(f.name)]
+    items.sort(key=ckpt_step)
+    for old in items[:-max_keep]:
+        try:
+            if old.is_dir():
+                shutil.rmtree(old)
+            else:
+                old.unlink()
+                md5 = Path(str(old) + ".md5")
+                if md5.exists():
+                    md5.unlink()
+        except FileNotFoundError:
+            pass

@@ -1,0 +1,125 @@
+"""Vanilla (single-file) checkpoints: ``ckpt_{step}.pt`` + optional ``.md5`` sidecar.
+
+API and file semantics follow reference pyrecover/checkpoint.py:25-215 (``save_ckpt_vanilla`` /
+``load_ckpt_vanilla``): rank 0 writes one ``torch.save``-loadable archive holding
+``{epoch, step, model, optimizer, lr_scheduler[, sampler_state]}`` with unprefixed model keys; the
+``.md5`` sidecar is the 32-hex md5 of the whole file; ``latest`` resolves to the newest ``*.pt``.
+
+Differences (all compatible with the reference's readers):
+* the archive is produced by the C++ engine from a pinned-memory snapshot (async optional), the
+  md5 is computed while writing, and the file appears atomically (tmp + fsync + rename);
+* a ``pyrecover_state`` entry carries RNG state and run metadata;
+* no model-device assert, no per-rank 3 s stagger, numeric retention (D7),
+  and ``module.``/``_orig_mod.`` prefixes are stripped on load (D12).
+"""
+from __future__ import annotations
+
+import logging
+import threading
+import time
+from pathlib import Path
+from typing import Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from .. import _ext
+from . import core
+from .serialization import plan_archive
+
+logger = logging.getLogger("pyrecover")
+
+
+def _device_of(model) -> torch.device:
+    for p in core.unwrap(model).parameters():
+        return p.device
+    return torch.device("cpu")
+
+
+def save_ckpt_vanilla(model, optimizer, lr_scheduler=None, sampler=None, step: int = 0, epoch: Optional[int] = None,
+                      checkpoint_path: str = "checkpoint.pt", max_keep: int = 3, verify: bool = True,
+                      is_distributed: bool = False, rank: int = 0, *, async_save: bool = False, fsync: bool = True,
+                      extra_state=None) -> str:
+    if is_distributed:
+        dist.barrier()
+    if rank == 0 or not is_distributed:
+        state = core.build_state(model, optimizer, lr_scheduler, sampler, step, epoch, extra_state)
+        ck = core.Checkpointer.get(_device_of(model))
+        staged = ck.stage(state)
+        prefix = Path(checkpoint_path).name
+        if prefix.endswith(".pt"):
+            prefix = prefix[:-3]
+        records, keep = plan_archive(staged, prefix or "archive")
+        base = Path(checkpoint_path).parent
+
+        def done(res, base=base, t0=time.perf_counter()):
+            core.apply_retention(base, max_keep, distributed=False)
+            logger.info(f"checkpoint {checkpoint_path}: {res['bytes'] / 2**30:.2f} GiB in {res['seconds']:.2f}s"
+                        + (f", md5 {res['md5']}" if verify else ""))
+
+        ck.write(str(checkpoint_path), [("zip", records)], verify, fsync, (staged, keep), done)
+        if not async_save:
+            ck.wait()
+    if is_distributed:
+        dist.barrier()
+    return str(checkpoint_path)
+
+
+def verify_checkpoint(path: str) -> Tuple[bool, str]:
+    """Compare the file's md5 with its ``.md5`` sidecar (streaming, native)."""
+    try:
+        want = Path(str(path) + ".md5").read_text().strip()
+        got = _ext.native().md5_file(str(path))
+        if want != got:
+            return False, f"Checksum mismatch for checkpoint {path}"
+        return True, ""
+    except Exception as e:
+        return False, str(e)
+
+
+def load_state_into(model, optimizer, lr_scheduler, sampler, ckpt) -> Tuple[int, int]:
+    m = core.unwrap(model)
+    sd = core.strip_prefixes(ckpt["model"])
+    with torch.no_grad():
+        missing, unexpected = m.load_state_dict(sd, strict=False)
+    if missing or unexpected:
+        raise RuntimeError(f"checkpoint/model key mismatch: missing={missing[:5]} unexpected={unexpected[:5]}")
+    if optimizer is not None and "optimizer" in ckpt:
+        optimizer.load_state_dict(ckpt["optimizer"])
+    if lr_scheduler is not None and "lr_scheduler" in ckpt:
+        lr_scheduler.load_state_dict(ckpt["lr_scheduler"])
+    if sampler is not None and "sampler_state" in ckpt and hasattr(sampler, "load_state_dict"):
+        sampler.load_state_dict(ckpt["sampler_state"])
+    ps = ckpt.get("pyrecover_state") or {}
+    core.restore_rng_state(ps.get("rng"))
+    return ckpt.get("epoch", 0), ckpt.get("step", 0)
+
+
+def load_ckpt_vanilla(model, optimizer, lr_scheduler=None, sampler=None, checkpoint_path: str = "latest",
+                      experiment_dir: str = ".", verify: bool = True, is_distributed: bool = False,
+                      rank: int = 0) -> Tuple[int, int]:
+    if is_distributed:
+        dist.barrier()
+    core.wait_all()
+    if checkpoint_path == "latest":
+        checkpoint_path = core.get_latest_checkpoint(str(experiment_dir))
+        if checkpoint_path is None:
+            raise RuntimeError(f"No checkpoint found in {experiment_dir}")
+    result = {"ok": True, "err": ""}
+    th = None
+    if verify and rank == 0:
+        def _v():
+            result["ok"], result["err"] = verify_checkpoint(checkpoint_path)
+        th = threading.Thread(target=_v, daemon=True)
+        th.start()
+    ckpt = torch.load(checkpoint_path, map_location="cpu", mmap=True, weights_only=True)
+    epoch, step = load_state_into(model, optimizer, lr_scheduler, sampler, ckpt)
+    del ckpt
+    if th is not None:
+        th.join()
+        if not result["ok"]:
+            raise RuntimeError(result["err"])
+    if is_distributed:
+        dist.barrier()
+    logger.info(f"Checkpoint loaded from {checkpoint_path} (epoch {epoch}, step {step})")
+    return epoch, step

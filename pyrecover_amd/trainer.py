@@ -1,0 +1,335 @@
+"""Training orchestrator (``train.py``): the reference's loop (reference train.py:37-400) on the
+MI355X engine.
+
+Same control flow, log lines, CSV, checkpoint naming/frequency and time-aware stop semantics as
+the reference, with these engine-level differences:
+
+* model: fused HIP ops + flat parameter/gradient buffers (:mod:`pyrecover_amd.models.llama`);
+* DDP: in-place bucketed RCCL all-reduce overlapped with backward (:mod:`.parallel.ddp`);
+* optimizer: one flat AdamW kernel (:mod:`.optim.adamw`);
+* data: resumable deterministic sampler whose cursor is checkpointed, tokenization
+  in DataLoader workers (D19), the batch after an epoch boundary is a real new batch (D6);
+* checkpoints: native engine, optionally asynchronous (snapshot fenced before the next optimizer
+  step), atomic files, streaming md5;
+* time-aware stop: the stop flag is only broadcast when time-aware checkpointing is on (D16),
+  signal-triggered stop and SLURM resubmission are available.
+"""
+from __future__ import annotations
+
+import csv
+import json
+import logging
+import os
+import random
+import time
+from pathlib import Path
+
+import torch
+from torch.utils.data import DataLoader
+
+from . import resubmit as resub
+from .ckpt import core as ckcore
+from .ckpt.sharded import finalize_pending, load_ckpt_distributed, save_ckpt_distributed
+from .ckpt.vanilla import load_ckpt_vanilla, save_ckpt_vanilla
+from .cli import PRECISION_STR_TO_DTYPE, set_default_dtype
+from .config import get_preset
+from .data.dataset import CollatorForCLM, ParquetDataset, SyntheticTokenDataset
+from .data.sampler import ResumableDistributedSampler
+from .data.tokenizer import load_tokenizer
+from .models.llama import Transformer
+from .optim.adamw import FlatAdamW
+from .optim.lr import build_lr_scheduler
+from .parallel import dist as D
+from .parallel.ddp import GradReducer, broadcast_flat
+from .timelimit import TimeAwareStopper, get_job_end_time
+from .utils.flops import num_flop_per_token
+from .utils.gemm_tuning import configure_gemm_tuning
+
+logger = logging.getLogger("pyrecover")
+log_rank0 = D.log_rank0
+
+
+def _profiler_start():
+    try:
+        torch.cuda.cudart().cudaProfilerStart()
+    except Exception:  # pragma: no cover
+        pass
+
+
+def _profiler_stop():
+    try:
+        torch.cuda.cudart().cudaProfilerStop()
+    except Exception:  # pragma: no cover
+        pass
+
+
+def train(args):
+    training_start_time = time.perf_counter()
+    total_checkpoint_store_time = 0.0
+    total_checkpoint_load_time = 0.0
+
+    local_rank, world_size = D.maybe_init_distributed(args.distributed)
+    rank = D.get_rank()
+    is_dist = world_size > 1
+    log_rank0(f"Experiment args: {args}")
+    use_cuda = torch.cuda.is_available()
+    device = torch.device("cuda", local_rank) if use_cuda else torch.device("cpu")
+    model_dtype = PRECISION_STR_TO_DTYPE[args.model_dtype]
+    torch.manual_seed(args.seed)
+    random.seed(args.seed)
+    configure_gemm_tuning(getattr(args, "gemm_tuning", "auto"))
+
+    # ---------------- data (reference train.py:53-84) ----------------
+    log_rank0("Setting up DataLoaders...")
+    seq_len = args.sequence_length
+    global_batch_size = int(args.batch_size)
+    local_batch_size = max(global_batch_size // world_size, 1)
+    n_samples = args.batch_size * args.training_steps
+    preset = get_preset(args.model_preset)
+    if args.synthetic_data:
+        vocab = args.vocab_size or preset.vocab_size
+        pad_id = 0
+        train_ds = SyntheticTokenDataset(vocab, seq_len, n_samples, seed=args.seed, pad_token_id=pad_id)
+    else:
+        tokenizer = load_tokenizer(args.tokenizer_name_or_path)
+        train_ds = ParquetDataset(args.dataset, tokenizer, seq_len, n_samples)
+        vocab = args.vocab_size or tokenizer.vocab_size
+        pad_id = tokenizer.pad_token_id
+    log_rank0(f"Global batch size: {global_batch_size}\nLocal batch size: {local_batch_size}")
+    train_sampler = ResumableDistributedSampler(len(train_ds), num_replicas=world_size, rank=rank, shuffle=True,
+                                                seed=args.seed)
+    train_collator = CollatorForCLM(seq_len, pad_id)
+    train_dl = DataLoader(train_ds, batch_size=local_batch_size, collate_fn=train_collator, sampler=train_sampler,
+                          num_workers=args.num_workers, pin_memory=use_cuda,
+                          persistent_workers=False)
+
+    # ---------------- model / parallelism / optimizer ----------------
+    log_rank0(f"Setting up Model ({args.model_preset})...")
+    model_config = get_preset(args.model_preset, seq_len=seq_len, vocab_size=vocab, n_layers=args.n_layers,
+                              use_flash_attention=args.use_flash_attention)
+    with set_default_dtype(model_dtype), torch.device(device):
+        model = Transformer(model_config)
+    flat = model.flatten_()
+    if args.compile:
+        log_rank0("--compile: the step already runs fused HIP kernels; Inductor/Triton is not used")
+    reducer = None
+    if is_dist:
+        broadcast_flat(flat)
+        reducer = GradReducer(flat, bucket_cap_mb=args.bucket_cap_mb)
+        log_rank0(f"DDP: {reducer.num_buckets} buckets, {sum(reducer.bucket_bytes()) / 2**30:.2f} GiB of gradients")
+    model.train()
+    optimizer = FlatAdamW(flat, lr=args.learning_rate, fused=args.fused_optimizer, grad_scale=1.0 / world_size)
+    lr_scheduler = build_lr_scheduler(optimizer, args.lr_warmup_steps)
+    num_flop_per_token_ = num_flop_per_token(model.num_params(exclude_embedding=True), model_config)
+    log_rank0(f"Model parameters: {model.num_params() / 1e9:.3f} B, FLOPs/token: {num_flop_per_token_ / 1e9:.2f} G")
+
+    ntokens_since_last_log = 0
+    ntraining_tokens_since_last_log = 0
+    time_last_log = time.perf_counter()
+
+    # ---------------- checkpoint dirs / CSV (reference train.py:135-161) ----------------
+    checkpoint_freq_steps = int(args.checkpoint_frequency)
+    ckpt_path = Path(args.checkpoint_dir)
+    if ckpt_path.exists() and not ckpt_path.is_dir():
+        raise SystemExit(f"Checkpoint dir {ckpt_path} exists as file already! Abort!")
+    exp_ckpt_path = ckpt_path / args.experiment_name
+    exp_ckpt_path.mkdir(parents=True, exist_ok=True)
+    csv_file = csv_writer = None
+    if args.log_loss_to_csv and D.is_rank0():
+        csv_path = exp_ckpt_path / f"{args.experiment_name}_loss_log.csv"
+        resume_csv = args.resume_from_checkpoint is not None and csv_path.exists()
+        csv_file = open(csv_path, "a" if resume_csv else "w", newline="")
+        csv_writer = csv.writer(csv_file)
+        if not resume_csv:
+            csv_writer.writerow(["Step", "Loss"])
+        csv_file.flush()
+    metrics_f = open(args.metrics_jsonl, "a") if (args.metrics_jsonl and D.is_rank0()) else None
+    if args.use_torch_distributed_ckpt:
+        log_rank0("Using sharded (torch.distributed.checkpoint-compatible) checkpointing")
+        save_ckpt_fn, load_ckpt_fn = save_ckpt_distributed, load_ckpt_distributed
+    else:
+        log_rank0("Using vanilla checkpointing")
+        save_ckpt_fn, load_ckpt_fn = save_ckpt_vanilla, load_ckpt_vanilla
+
+    def ckpt_name(step, final=False):
+        suffix = "_final" if final else ""
+        return exp_ckpt_path / (f"ckpt_{step}{suffix}" if args.use_torch_distributed_ckpt else f"ckpt_{step}{suffix}.pt")
+
+    def do_save(step, epoch, final=False):
+        p = ckpt_name(step, final)
+        t0 = time.perf_counter()
+        save_ckpt_fn(model, optimizer, lr_scheduler, train_sampler, step, epoch, p,
+                     max_keep=args.max_kept_checkpoints, verify=args.verify_checkpoints, is_distributed=is_dist,
+                     rank=rank, async_save=(args.async_checkpoint and not final), fsync=not args.no_fsync)
+        if final:
+            ckcore.wait_all()
+            if args.use_torch_distributed_ckpt:
+                finalize_pending()
+        return p, time.perf_counter() - t0
+
+    # ---------------- time-aware (reference train.py:163-190) ----------------
+    stopper = None
+    if args.timeaware_checkpointing:
+        stopper = TimeAwareStopper(args.default_iter_time, args.default_ckpt_time, end_time=get_job_end_time(),
+                                   install_signals=args.handle_signals)
+        log_rank0(f"Initial max_iter_time: {stopper.max_iter}, max_ckpt_time: {stopper.max_ckpt}, "
+                  f"buffer_time: {stopper.buffer}")
+        if stopper.end_time is None:
+            log_rank0("Warning: SLURM_JOB_END_TIME is not set. Time-check logic will be skipped.")
+        log_rank0(f"SLURM_JOB_END_TIME: {stopper.end_time}")
+    if args.resubmit != "none":
+        resub.setup_resubmission(args.resubmit, args.resubmit_script,
+                                 [a for a in os.environ.get("PYRECOVER_SCRIPT_ARGS", "").split() if a])
+
+    # ---------------- resume (reference train.py:192-212) ----------------
+    train_step = 0
+    epoch = 1
+    train_sampler.set_epoch(epoch)
+    if args.resume_from_checkpoint is not None:
+        log_rank0(f"Try resume from checkpoint {args.resume_from_checkpoint}")
+        t0 = time.perf_counter()
+        epoch, train_step = load_ckpt_fn(model, optimizer, lr_scheduler, train_sampler, args.resume_from_checkpoint,
+                                         experiment_dir=exp_ckpt_path, verify=args.verify_checkpoints,
+                                         is_distributed=is_dist, rank=rank)
+        epoch = epoch or 1
+        dt = time.perf_counter() - t0
+        total_checkpoint_load_time += dt
+        log_rank0(f"Checkpoint loading completed in {dt:.2f} seconds")
+    D.barrier()
+
+    train_dl_iterator = iter(train_dl)
+    should_stop = False
+    stop_flag = torch.zeros(1, dtype=torch.int32, device=device)
+    log_rank0("Starting training!")
+    loss = None
+    while train_step < args.training_steps:
+        train_step += 1
+        if stopper is not None and D.is_rank0() and stopper.should_stop():
+            should_stop = True
+            rem = stopper.remaining()
+            log_rank0(f"[TIME CHECK] Remaining time ({rem if rem is not None else float('nan'):.2f}s) < threshold "
+                      f"({stopper.threshold:.2f}s). should_stop set to True.")
+        iter_start = time.perf_counter()
+        if args.profile and args.profile_step_start == train_step:
+            _profiler_start()
+        if args.profile and args.profile_step_start <= train_step <= args.profile_step_end:
+            torch.cuda.nvtx.range_push(f"step_{train_step}") if use_cuda else None
+
+        train_sampler.set_epoch(epoch)
+        try:
+            input_ids, labels = next(train_dl_iterator)
+        except StopIteration:
+            epoch += 1
+            train_sampler.set_epoch(epoch)
+            train_dl_iterator = iter(train_dl)
+            input_ids, labels = next(train_dl_iterator)
+        train_sampler.advance(input_ids.shape[0])
+
+        ntokens_since_last_log += global_batch_size * seq_len
+        num_items_in_batch = labels.ne(-100).sum()
+        ntraining_tokens_since_last_log += int(num_items_in_batch) * world_size
+        input_ids = input_ids.to(device, non_blocking=True)
+        labels = labels.to(device, non_blocking=True)
+
+        optimizer.zero_grad()
+        loss = model(input_ids, labels=labels)
+        loss.backward()
+        if reducer is not None:
+            reducer.finish()
+        if args.clip_grad:
+            optimizer.grad_scale_dev = _clip_coef(flat, args.grad_max_norm, 1.0 / world_size)
+        ckcore.fence_all()  # an async snapshot must land before parameters change
+        optimizer.step()
+        lr_scheduler.step()
+
+        if csv_writer is not None:
+            csv_writer.writerow([train_step, loss.item()])
+            csv_file.flush()
+
+        if train_step == 1 or train_step % args.logging_frequency == 0:
+            time_delta = time.perf_counter() - time_last_log
+            tps = ntokens_since_last_log / time_delta
+            per_gpu = tps / world_size
+            mfu = 100 * num_flop_per_token_ * per_gpu / (args.peak_tflops * 1e12)
+            tflops = num_flop_per_token_ * per_gpu / 1e12
+            training_tps = ntraining_tokens_since_last_log / time_delta
+            lval = loss.item()
+            log_rank0(f"Epoch: {epoch} | Step: {train_step} | Loss: {lval:.2f} | Tokens per second: {tps:.2f} | "
+                      f"Training tokens per second (%): {100 * training_tps / tps:.2f} | MFU (%): {mfu:.2f} | "
+                      f"TFLOPs: {tflops:.2f} | Tokens per second per GPU: {per_gpu:.2f}")
+            if metrics_f is not None:
+                metrics_f.write(json.dumps({"step": train_step, "epoch": epoch, "loss": lval, "tokens_per_s": tps,
+                                            "tokens_per_s_per_gpu": per_gpu, "mfu_pct": mfu, "tflops_per_gpu": tflops,
+                                            "time": time.time()}) + "\n")
+                metrics_f.flush()
+            ntokens_since_last_log = 0
+            ntraining_tokens_since_last_log = 0
+            time_last_log = time.perf_counter()
+
+        if stopper is not None:
+            iter_time = time.perf_counter() - iter_start
+            if stopper.update_iter(iter_time):
+                log_rank0(f"Updated max_iter_time: {stopper.max_iter}")
+            if train_step % args.logging_frequency == 0:
+                log_rank0(f"Current buffer_time: {stopper.buffer}")
+
+        if checkpoint_freq_steps != -1 and train_step % checkpoint_freq_steps == 0:
+            log_rank0(f"Saving checkpoint to {ckpt_name(train_step)}")
+            _, store_time = do_save(train_step, epoch)
+            total_checkpoint_store_time += store_time
+            if stopper is not None and stopper.update_ckpt(store_time):
+                log_rank0(f"Updated max_ckpt_time: {stopper.max_ckpt}")
+            log_rank0(f"Checkpoint store completed in {store_time:.2f} seconds")
+
+        if stopper is not None and is_dist:
+            stop_flag.fill_(1 if (should_stop or stopper.signaled) else 0)
+            torch.distributed.broadcast(stop_flag, src=0)
+            should_stop = bool(stop_flag.item())
+        elif stopper is not None and stopper.signaled:
+            should_stop = True
+
+        if getattr(args, "stop_at_step", None) is not None and train_step == args.stop_at_step:
+            should_stop = True
+            if stopper is None:
+                stopper = TimeAwareStopper(args.default_iter_time, args.default_ckpt_time, end_time=None)
+        if stopper is not None and should_stop:
+            log_rank0(f"[TIME CHECK] Saving final checkpoint to {ckpt_name(train_step, True)} before exit.")
+            _, store_time = do_save(train_step, epoch, final=True)
+            total_checkpoint_store_time += store_time
+            log_rank0(f"[TIME CHECK] Final checkpoint store completed in {store_time:.2f} seconds")
+            if args.resubmit != "none":
+                resub.maybe_resubmit(rank)
+            break
+
+        if args.profile and args.profile_step_start <= train_step <= args.profile_step_end and use_cuda:
+            torch.cuda.nvtx.range_pop()
+        if args.profile and args.profile_step_end == train_step:
+            _profiler_stop()
+
+    # drain background checkpoint writes before reporting
+    t0 = time.perf_counter()
+    ckcore.wait_all()
+    finalize_pending()
+    total_checkpoint_store_time += time.perf_counter() - t0
+    total_training_time = time.perf_counter() - training_start_time
+    if csv_file is not None:
+        csv_file.close()
+    if metrics_f is not None:
+        metrics_f.close()
+    log_rank0(f"Training completed in {total_training_time:.2f} seconds")
+    log_rank0(f"Total checkpoint loading time: {total_checkpoint_load_time:.2f} seconds")
+    log_rank0(f"Total checkpoint storing time: {total_checkpoint_store_time:.2f} seconds")
+    log_rank0(f"Total checkpointing time: {(total_checkpoint_load_time + total_checkpoint_store_time):.2f} seconds")
+    D.maybe_cleanup_distributed()
+    return {"step": train_step, "epoch": epoch, "loss": float(loss.item()) if loss is not None else None,
+            "stopped_early": should_stop}
+
+
+def _clip_coef(flat, max_norm: float, pre_scale: float):
+    """Device-side clip coefficient min(1, max_norm / ||g||) over the flat (reduced) gradient."""
+    if flat.grad.is_cuda:
+        from . import _ext
+
+        return _ext.native().grad_norm(flat.grad, max_norm, pre_scale)[1:2]
+    norm = flat.grad.float().norm() * pre_scale
+    return torch.clamp(max_norm / (norm + 1e-6), max=1.0).reshape(1)
