@@ -147,6 +147,8 @@ def main():
             "model_tflops_per_gpu": round(fpt * tps / world / 1e12, 2),
             "mfu_pct_vs_2.5PF": round(100 * fpt * tps / world / 2.5e15, 2),
             "final_loss": round(final_loss, 4),
+            "peak_mem_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1),
+            "gemm_table": bool(torch.cuda.tunable.is_enabled()),
         }
         print(json.dumps(out), flush=True)
     from pyrecover_amd.utils.gemm_tuning import flush_tuning

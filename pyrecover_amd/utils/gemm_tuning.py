@@ -41,7 +41,9 @@ def configure_gemm_tuning(mode: str = "auto", table: str = TABLE) -> bool:
 
 
 def flush_tuning():
+    """TunableOp writes its table when the process exits; newer torch versions can flush early."""
     import torch
 
-    if torch.cuda.is_available() and torch.cuda.tunable.is_enabled() and torch.cuda.tunable.tuning_is_enabled():
-        torch.cuda.tunable.write_file()
+    t = torch.cuda.tunable
+    if torch.cuda.is_available() and t.is_enabled() and t.tuning_is_enabled() and hasattr(t, "write_file"):
+        t.write_file()
