@@ -34,6 +34,8 @@ def parse():
     ap.add_argument("--lr", type=float, default=1e-5)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--profile-steps", type=int, default=0, help="emit roctx ranges for this many steps")
+    ap.add_argument("--no-overlap-optimizer", action="store_true",
+                    help="AdamW after backward instead of per bucket during backward")
     ap.add_argument("--gemm-tuning", choices=["auto", "off", "tune"], default="auto",
                     help="hipBLASLt solution table (tuning/): auto = use the committed table if present")
     return ap.parse_args()
@@ -73,11 +75,12 @@ def main():
         model = Transformer(cfg)
         torch.set_default_dtype(prev)
     flat = model.flatten_()
-    reducer = None
     if world > 1:
         broadcast_flat(flat)
-        reducer = GradReducer(flat, bucket_cap_mb=args.bucket_mb)
+    reducer = GradReducer(flat, bucket_cap_mb=args.bucket_mb)
     opt = FlatAdamW(flat, lr=args.lr, fused=True, grad_scale=1.0 / world)
+    if not args.no_overlap_optimizer:
+        opt.enable_overlap(reducer)
     sched = build_lr_scheduler(opt, 10)
 
     B, S = args.batch_per_gpu, args.seq_len
@@ -93,8 +96,7 @@ def main():
         opt.zero_grad()
         loss = model(x, labels=y)
         loss.backward()
-        if reducer is not None:
-            reducer.finish()
+        reducer.finish()
         opt.step()
         sched.step()
         return loss
@@ -142,7 +144,7 @@ def main():
             "data": "synthetic (uniform random token ids), random-init weights",
             "config": {"model": f"{args.model}-shape ({n_params / 1e9:.2f}B params)", "global_batch": B * world,
                        "seq_len": S, "parallelism": f"dp{world}", "batch_per_gpu": B,
-                       "bucket_mb": args.bucket_mb if world > 1 else None, "optimizer": "AdamW (flat fused HIP)"},
+                       "bucket_mb": args.bucket_mb if world > 1 else None, "optimizer": "AdamW (flat fused HIP)" + ("" if args.no_overlap_optimizer else ", overlapped with backward")},
             "tokens_per_sec_per_gpu": round(tps / world, 2),
             "model_tflops_per_gpu": round(fpt * tps / world / 1e12, 2),
             "mfu_pct_vs_2.5PF": round(100 * fpt * tps / world / 2.5e15, 2),

@@ -88,6 +88,8 @@ def build_parser() -> argparse.ArgumentParser:
                    help="snapshot to pinned host memory and write in the background while training continues")
     p.add_argument("--no-fsync", action="store_true", help="skip fsync of checkpoint files")
     p.add_argument("--clip-grad", action="store_true", help="enable gradient clipping at --grad-max-norm")
+    p.add_argument("--no-overlap-optimizer", action="store_true",
+                   help="run AdamW after backward instead of per gradient bucket during backward")
     p.add_argument("--resubmit", choices=["none", "requeue", "chain"], default="none",
                    help="after a time-aware final checkpoint, requeue/chain the SLURM job")
     p.add_argument("--resubmit-script", type=str, default=None)

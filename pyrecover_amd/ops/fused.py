@@ -212,8 +212,10 @@ class _AttentionBlock(torch.autograd.Function):
         nq, nk = Hq * D, Hkv * D
         dy2 = dy.reshape(T, -1)
         o2 = o.view(T, nq)
-        slot_o.mm_(dy2.t(), o2, tuple(w_o.shape))
+        # every read of a weight is enqueued BEFORE its gradient slot is published: a published
+        # slot may be updated by the optimizer (overlapped with backward) on another stream.
         do = torch.mm(dy2, w_o).view(B, S, Hq, D)
+        slot_o.mm_(dy2.t(), o2, tuple(w_o.shape))
         dqkv = torch.empty_like(qkv)
         q = qkv[:, :nq].view(B, S, Hq, D)
         k = qkv[:, nq:nq + nk].view(B, S, Hkv, D)
@@ -226,8 +228,8 @@ class _AttentionBlock(torch.autograd.Function):
             _ext.require_for(dqkv).rope_(dqkv, nq + nk, tab, D, S, 0, True)
         else:
             ref.rope_inplace_2d(dqkv, nq + nk, tab, D, S, inverse=True)
-        slot_qkv.mm_(dqkv.t(), x2, tuple(w_qkv.shape))
         dx = torch.mm(dqkv, w_qkv)
+        slot_qkv.mm_(dqkv.t(), x2, tuple(w_qkv.shape))
         n_params = ctx.needs_input_grad.__len__() - 7
         return (dx.view(B, S, -1), None, None, None, None, None, None) + (None,) * n_params
 
@@ -275,11 +277,11 @@ class _SwiGLUMLP(torch.autograd.Function):
         slot13, slot2 = ctx.slots
         shape = dy.shape
         dy2 = dy.reshape(-1, shape[-1])
-        slot2.mm_(dy2.t(), a, tuple(w2.shape))
         da = torch.mm(dy2, w2)
+        slot2.mm_(dy2.t(), a, tuple(w2.shape))
         dgu = _swiglu_bwd_(da, gu)  # in place over gu (dead after this)
-        slot13.mm_(dgu.t(), x2, tuple(w13.shape))
         dx = torch.mm(dgu, w13)
+        slot13.mm_(dgu.t(), x2, tuple(w13.shape))
         n_params = len(ctx.needs_input_grad) - 5
         return (dx.view(shape), None, None, None, None) + (None,) * n_params
 
@@ -326,8 +328,8 @@ class _LinearCrossEntropy(torch.autograd.Function):
             p[torch.arange(lab.numel()), lab.clamp_min(0)] -= valid.float()
             p = p * valid.float().unsqueeze(1) * (dloss.float() / n)
             dlogits = p.to(logits.dtype)
-        ctx.slot.mm_(dlogits.t(), h2, tuple(w_out.shape))
         dh = torch.mm(dlogits, w_out)
+        ctx.slot.mm_(dlogits.t(), h2, tuple(w_out.shape))
         return dh.view(ctx.hshape), None, None, None, None, None
 
 

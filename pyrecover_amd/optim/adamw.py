@@ -39,6 +39,57 @@ class FlatAdamW(torch.optim.AdamW):
         self.exp_avg_sq = torch.zeros_like(flat.data)
         self._step = 0
         self._bind_state()
+        self.overlap = False
+        self._in_step = False
+        self._done_ranges = []
+        self.pre_update_fences = []  # callables run on the update stream before any update
+
+    # --- overlapped update (optimizer-in-backward) ----------------------------------------
+    def enable_overlap(self, reducer):
+        """Update each gradient bucket as soon as it is reduced, on a side stream, overlapped with
+        the rest of the backward pass. Math and result are identical to :meth:`step`."""
+        self.overlap = True
+        self.reducer = reducer
+        reducer.hooks.append(self._on_bucket)
+        self.stream = torch.cuda.Stream(device=self.flat.data.device) if self.flat.data.is_cuda else None
+
+    def _coeffs(self):
+        g = self.param_groups[0]
+        b1, b2 = g["betas"]
+        lr, eps, wd = float(g["lr"]), float(g["eps"]), float(g["weight_decay"])
+        return lr, b1, b2, eps, wd, 1.0 - b1 ** self._step, math.sqrt(1.0 - b2 ** self._step)
+
+    def _update_range(self, lo, hi):
+        f = self.flat
+        lr, b1, b2, eps, wd, bc1, bc2_sqrt = self._coeffs()
+        if f.data.is_cuda:
+            _ext.require_for(f.data).adamw_flat_(f.data[lo:hi], f.grad[lo:hi], self.exp_avg[lo:hi],
+                                                 self.exp_avg_sq[lo:hi], lr, b1, b2, eps, wd, bc1, bc2_sqrt,
+                                                 self.grad_scale, self.grad_scale_dev)
+        else:
+            self._step_reference(lr, b1, b2, eps, wd, bc1, bc2_sqrt, lo, hi)
+
+    def _on_bucket(self, b, lo, hi, work):
+        if not self.overlap or self.grad_scale_dev is not None:
+            return  # clipping needs the global norm first: fall back to step()
+        if not self._in_step:
+            self._in_step = True
+            self._step += 1
+        if self.stream is None:
+            if work is not None:
+                work.wait()
+            self._update_range(lo, hi)
+        else:
+            ev = torch.cuda.Event()
+            ev.record()  # compute stream: every read of these weights is already enqueued
+            with torch.cuda.stream(self.stream):
+                self.stream.wait_event(ev)
+                if work is not None:
+                    work.wait()  # update stream waits for the bucket's all-reduce
+                for fence in self.pre_update_fences:
+                    fence()
+                self._update_range(lo, hi)
+        self._done_ranges.append((lo, hi))
 
     def _bind_state(self):
         for p in self.param_groups[0]["params"]:
@@ -54,6 +105,9 @@ class FlatAdamW(torch.optim.AdamW):
     def zero_grad(self, set_to_none: bool = True):
         """Marks gradient slots fresh; the flat gradient views are never set to None."""
         self.flat.zero_grad()
+        if self.overlap and self.stream is not None:
+            # the next backward overwrites gradients the update stream may still be reading
+            torch.cuda.current_stream(self.flat.data.device).wait_stream(self.stream)
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -61,6 +115,15 @@ class FlatAdamW(torch.optim.AdamW):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        if self.overlap and self.grad_scale_dev is None:
+            self.reducer.finish()  # launches (and so updates) any bucket not yet ready
+            if not self._in_step:  # no bucket fired (no backward this step)
+                self._step += 1
+            if self.stream is not None:
+                torch.cuda.current_stream(self.flat.data.device).wait_stream(self.stream)
+            self._in_step = False
+            self._done_ranges = []
+            return loss
         g = self.param_groups[0]
         self._step += 1
         b1, b2 = g["betas"]
@@ -75,21 +138,23 @@ class FlatAdamW(torch.optim.AdamW):
             self._step_reference(lr, b1, b2, eps, wd, bc1, bc2_sqrt)
         return loss
 
-    def _step_reference(self, lr, b1, b2, eps, wd, bc1, bc2_sqrt):
+    def _step_reference(self, lr, b1, b2, eps, wd, bc1, bc2_sqrt, lo=0, hi=None):
         f = self.flat
+        hi = f.numel if hi is None else hi
         gs = self.grad_scale * (float(self.grad_scale_dev[0]) if self.grad_scale_dev is not None else 1.0)
-        p = f.data.float()
-        gr = f.grad.float() * gs
-        m = self.exp_avg.float()
-        v = self.exp_avg_sq.float()
+        pd, gd, md, vd = f.data[lo:hi], f.grad[lo:hi], self.exp_avg[lo:hi], self.exp_avg_sq[lo:hi]
+        p = pd.float()
+        gr = gd.float() * gs
+        m = md.float()
+        v = vd.float()
         p.mul_(1 - lr * wd)
         m.lerp_(gr, 1 - b1)
         v.mul_(b2).addcmul_(gr, gr, value=1 - b2)
         denom = v.sqrt().div_(bc2_sqrt).add_(eps)
         p.addcdiv_(m, denom, value=-(lr / bc1))
-        f.data.copy_(p)
-        self.exp_avg.copy_(m)
-        self.exp_avg_sq.copy_(v)
+        pd.copy_(p)
+        md.copy_(m)
+        vd.copy_(v)
 
     # --- checkpoint compatibility -------------------------------------------------------
     def state_dict(self):

@@ -14,6 +14,11 @@ train.py:107-115 and its Reducer).
 * The gradient is SUM-reduced; the 1/world_size average is folded into the optimizer kernel
   (``FlatAdamW.grad_scale``), so there is no separate scaling pass.
 * Deterministic: identical bucket order/boundaries on every rank and every step.
+* With ``world_size == 1`` (or no process group) the same bucket machinery runs without
+  communication, so bucket hooks (the overlapped optimizer) work identically on one GPU.
+* Bucket hooks ``fn(bucket, lo, hi, work)`` run right after a bucket is launched; the
+  overlapped AdamW (:meth:`pyrecover_amd.optim.adamw.FlatAdamW.enable_overlap`) uses them to
+  update each bucket's parameters on a side stream while backward continues.
 """
 from __future__ import annotations
 
@@ -29,7 +34,8 @@ class GradReducer:
     def __init__(self, flat: FlatParams, group=None, bucket_cap_mb: float = 256.0, first_bucket_mb: float = 64.0):
         self.flat = flat
         self.group = group
-        self.world = dist.get_world_size(group)
+        self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+        self.hooks = []
         esz = flat.grad.element_size()
         cap = int(bucket_cap_mb * 2 ** 20 / esz)
         first_cap = int(first_bucket_mb * 2 ** 20 / esz)
@@ -88,8 +94,12 @@ class GradReducer:
 
     def _launch(self, b: int):
         lo, hi = self.ranges[b]
-        self.works[b] = dist.all_reduce(self.flat.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
-                                        async_op=True)
+        work = None
+        if self.world > 1:
+            work = dist.all_reduce(self.flat.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        self.works[b] = work
+        for h in self.hooks:
+            h(b, lo, hi, work)
 
     def finish(self):
         """Launch any bucket whose slots were not all produced (unused params), then make the

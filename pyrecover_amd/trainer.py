@@ -112,13 +112,19 @@ def train(args):
     flat = model.flatten_()
     if args.compile:
         log_rank0("--compile: the step already runs fused HIP kernels; Inductor/Triton is not used")
+    overlap = not (args.clip_grad or args.no_overlap_optimizer)
     reducer = None
     if is_dist:
         broadcast_flat(flat)
+    if is_dist or overlap:
         reducer = GradReducer(flat, bucket_cap_mb=args.bucket_cap_mb)
-        log_rank0(f"DDP: {reducer.num_buckets} buckets, {sum(reducer.bucket_bytes()) / 2**30:.2f} GiB of gradients")
+        log_rank0(f"Gradient buckets: {reducer.num_buckets}, {sum(reducer.bucket_bytes()) / 2**30:.2f} GiB"
+                  f"{' (RCCL all-reduce)' if is_dist else ''}")
     model.train()
     optimizer = FlatAdamW(flat, lr=args.learning_rate, fused=args.fused_optimizer, grad_scale=1.0 / world_size)
+    if overlap:
+        optimizer.enable_overlap(reducer)
+        optimizer.pre_update_fences.append(ckcore.fence_all)
     lr_scheduler = build_lr_scheduler(optimizer, args.lr_warmup_steps)
     num_flop_per_token_ = num_flop_per_token(model.num_params(exclude_embedding=True), model_config)
     log_rank0(f"Model parameters: {model.num_params() / 1e9:.3f} B, FLOPs/token: {num_flop_per_token_ / 1e9:.2f} G")

@@ -53,3 +53,44 @@ def test_model_grads_vs_fp32_reference(cuda, preset):
         g, r = p.grad.float().cpu(), gref[n]
         rel = ((g - r).norm() / r.norm().clamp_min(1e-12)).item()
         assert rel < 5e-2, (n, rel)
+
+
+def _train_steps(cuda, overlap, steps=3, preset="llama-tiny", seed=0):
+    from pyrecover_amd.optim.adamw import FlatAdamW
+    from pyrecover_amd.parallel.ddp import GradReducer
+
+    torch.manual_seed(seed)
+    a = get_preset(preset, seq_len=256)
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.bfloat16)
+    with torch.device(cuda):
+        m = Transformer(a)
+    torch.set_default_dtype(prev)
+    flat = m.flatten_()
+    red = GradReducer(flat, bucket_cap_mb=0.5, first_bucket_mb=0.25)
+    opt = FlatAdamW(flat, lr=1e-3)
+    if overlap:
+        opt.enable_overlap(red)
+    g = torch.Generator(device=cuda)
+    g.manual_seed(123)
+    for _ in range(steps):
+        t = torch.randint(0, a.vocab_size, (2, 257), device=cuda, generator=g)
+        opt.zero_grad()
+        m(t[:, :-1], labels=t[:, 1:]).backward()
+        red.finish()
+        opt.step()
+    torch.cuda.synchronize()
+    return flat.data.clone(), opt.exp_avg_sq.clone(), red.num_buckets
+
+
+def test_overlapped_optimizer_is_bit_identical(cuda):
+    p0, v0, nb = _train_steps(cuda, overlap=False)
+    p1, v1, _ = _train_steps(cuda, overlap=True)
+    assert nb > 3
+    assert torch.equal(p0, p1) and torch.equal(v0, v1)
+
+
+def test_training_is_deterministic(cuda):
+    p0, _, _ = _train_steps(cuda, overlap=True, seed=5)
+    p1, _, _ = _train_steps(cuda, overlap=True, seed=5)
+    assert torch.equal(p0, p1)
