@@ -200,6 +200,7 @@ class Checkpointer:
         os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
         self.engine.write_items(str(path), items, md5, fsync)
         self.pending = Job(self, str(path), keepalive, on_done)
+        _maybe_inject_fault("during_write", path)
         return self.pending
 
     def busy(self) -> bool:
@@ -247,6 +248,22 @@ def fence_all():
 
 
 # ------------------------------------------------------------------------------------------
+def _maybe_inject_fault(point: str, path: str):
+    """Fault injection for recovery tests: ``PYRECOVER_FAULT=kill_during_write[:<substring>]``
+    SIGKILLs this process right after a checkpoint write to a matching path has started (the
+    archive is still a ``.tmp`` file), emulating a node failure / hard preemption mid-save."""
+    spec = os.environ.get("PYRECOVER_FAULT", "")
+    if not spec.startswith("kill_" + point):
+        return
+    _, _, match = spec.partition(":")
+    if match and match not in str(path):
+        return
+    import signal
+
+    time.sleep(0.01)
+    os.kill(os.getpid(), signal.SIGKILL)
+
+
 _STEP_RE = re.compile(r"ckpt_(\d+)(_final)?")
 
 

@@ -1,0 +1,202 @@
+"""CPU tests of the framework around the kernels: CLI parity, data, sampler, LR schedule,
+time-aware stop (fake clock), resubmission, retention/latest, tools, fault injection."""
+import os
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+import pytest
+import torch
+
+ROOT = Path(__file__).resolve().parents[1]
+
+REFERENCE_FLAGS = {  # flag -> reference default (reference utils.py:105-261)
+    "dataset": "/capstor/store/cscs/ethz/large-sc/datasets/train_data.parquet",
+    "tokenizer_name_or_path": "unsloth/Mistral-Nemo-Base-2407-bnb-4bit",
+    "sequence_length": 2048, "batch_size": 1, "fused_optimizer": False, "learning_rate": 1e-5,
+    "lr_warmup_steps": 10, "training_steps": 1000, "logging_frequency": 5, "profile": False,
+    "profile_step_start": 10, "profile_step_end": 12, "grad_max_norm": 1, "model_dtype": "bf16",
+    "compile": False, "distributed": False, "checkpoint_dir": "checkpoints/", "checkpoint_frequency": 10,
+    "resume_from_checkpoint": None, "experiment_name": "default-exp", "verify_checkpoints": False,
+    "max_kept_checkpoints": 3, "use_torch_distributed_ckpt": False, "default_iter_time": 1.0,
+    "default_ckpt_time": 10.0, "timeaware_checkpointing": False, "use_flash_attention": False,
+    "log_loss_to_csv": False,
+}
+
+
+def test_cli_has_every_reference_flag_with_same_default():
+    from pyrecover_amd.cli import get_args
+
+    a = get_args([])
+    for k, v in REFERENCE_FLAGS.items():
+        assert getattr(a, k) == v, k
+    a = get_args(["--experiment_name", "x", "--use_flash_attention", "--resume-from-checkpoint", "latest",
+                  "--use-torch-distributed-ckpt", "--timeaware-checkpointing", "--model-dtype", "fp16"])
+    assert a.experiment_name == "x" and a.use_flash_attention and a.resume_from_checkpoint == "latest"
+    assert len(REFERENCE_FLAGS) == 28
+
+
+def test_param_count_matches_reference_default():
+    sys.path.insert(0, str(ROOT))
+    import test_model
+
+    assert test_model.main() == 8_053_329_920  # SURVEY §6 (derived from the reference model)
+
+
+def test_lr_schedule_matches_reference():
+    from pyrecover_amd.optim.lr import linear_warmup_constant
+
+    assert [linear_warmup_constant(10, s) for s in (0, 4, 9, 10, 100)] == [1 / 11, 5 / 11, 10 / 11, 1, 1]
+
+
+def test_collator_and_parquet_dataset(tmp_path):
+    from pyrecover_amd.data.dataset import CollatorForCLM, ParquetDataset, make_synthetic_parquet
+    from pyrecover_amd.data.tokenizer import ByteTokenizer
+
+    p = make_synthetic_parquet(str(tmp_path / "d.parquet"), n_docs=5, min_words=1, max_words=40)
+    tok = ByteTokenizer()
+    ds = ParquetDataset(p, tok, 64, 12)
+    assert len(ds) == 12
+    assert ds[7]["input_ids"] == ds[2]["input_ids"]  # idx % real_length
+    x, y = CollatorForCLM(64, tok.pad_token_id)([ds[i] for i in range(3)])
+    assert x.shape == y.shape == (3, 64)
+    assert ((y == -100) | (y != tok.pad_token_id)).all()
+    full = torch.tensor([ds[0]["input_ids"]])
+    assert torch.equal(x[0], full[0, :-1])
+
+
+def test_sampler_is_deterministic_sharded_and_resumable():
+    from pyrecover_amd.data.sampler import ResumableDistributedSampler
+
+    s0 = ResumableDistributedSampler(10, 2, 0, seed=3)
+    s1 = ResumableDistributedSampler(10, 2, 1, seed=3)
+    a, b = list(s0), list(s1)
+    assert sorted(a + b) == list(range(10))
+    s0.advance(3)
+    st = s0.state_dict()
+    s2 = ResumableDistributedSampler(10, 2, 0, seed=3)
+    s2.load_state_dict(st)
+    assert list(s2) == a[3:]
+    s2.set_epoch(1)
+    assert list(s2) != a and s2.cursor == 0
+    assert hasattr(s0, "set_state")  # stored under the reference's "sampler_state" key
+
+
+def test_timeaware_stopper_reference_thresholds():
+    from pyrecover_amd.timelimit import TimeAwareStopper
+
+    now = [1000.0]
+    st = TimeAwareStopper(1.0, 10.0, end_time=1100.0, clock=lambda: now[0])
+    assert st.threshold == 1 + 10 + (10 * 1 + 2 * 10)  # 41 s initially
+    assert not st.should_stop()
+    st.update_iter(3.0)
+    assert st.buffer == 5 * 3 + 10 and st.threshold == 3 + 10 + 25
+    now[0] = 1100 - 37.9
+    assert st.should_stop()
+    st2 = TimeAwareStopper(1.0, 10.0, end_time=None)
+    assert not st2.should_stop()
+    st2.signaled = True
+    assert st2.should_stop()
+
+
+def test_timeaware_training_stops_and_resumes(tmp_path, monkeypatch):
+    from pyrecover_amd.cli import get_args
+    from pyrecover_amd.trainer import train
+
+    # a job that "ends" in 30 s: below the 41 s initial threshold at step 1
+    monkeypatch.setenv("SLURM_JOB_END_TIME", str(time.time() + 30))
+    base = ["--model-preset", "llama-micro", "--synthetic-data", "--sequence-length", "128", "--batch-size", "2",
+            "--training-steps", "50", "--checkpoint-dir", str(tmp_path), "--checkpoint-frequency", "-1",
+            "--model-dtype", "fp32", "--num-workers", "0", "--timeaware-checkpointing", "--verify-checkpoints"]
+    r = train(get_args(base))
+    assert r["stopped_early"] and r["step"] == 1
+    final = tmp_path / "default-exp" / "ckpt_1_final.pt"
+    assert final.exists() and Path(str(final) + ".md5").exists()
+    monkeypatch.delenv("SLURM_JOB_END_TIME")
+    r = train(get_args(base[:-2] + ["--training-steps", "3", "--resume-from-checkpoint", "latest"]))
+    assert r["step"] == 3 and not r["stopped_early"]
+
+
+def test_slurm_duration_parse_and_remaining(monkeypatch):
+    from pyrecover_amd.timelimit import _parse_slurm_duration, get_remaining_time
+
+    assert _parse_slurm_duration("1-02:03:04") == 86400 + 7384
+    assert _parse_slurm_duration("39:30") == 2370
+    assert _parse_slurm_duration("UNLIMITED") is None
+    monkeypatch.setenv("SLURM_JOB_END_TIME", "2000")
+    assert get_remaining_time(now=1500) == 500
+
+
+def test_resubmit_commands():
+    from pyrecover_amd.resubmit import ResubmitConfig, resubmit_command
+
+    env = {"SLURM_JOB_ID": "77"}
+    assert resubmit_command(ResubmitConfig("requeue"), env) == ["scontrol", "requeue", "77"]
+    cmd = resubmit_command(ResubmitConfig("chain", "run.sh", ["--continue"]), env)
+    assert cmd[:2] == ["sbatch", "--dependency=afterany:77"] and cmd[-2:] == ["run.sh", "--continue"]
+    assert resubmit_command(ResubmitConfig("requeue"), {}) is None
+    assert resubmit_command(ResubmitConfig("requeue", max_resubmits=2),
+                            {"SLURM_JOB_ID": "1", "PYRECOVER_RESUBMIT_COUNT": "2"}) is None
+
+
+def test_retention_is_numeric_and_latest_skips_incomplete(tmp_path):
+    from pyrecover_amd.ckpt.core import apply_retention, get_latest_checkpoint
+
+    for s in (2000, 10000, 300):
+        (tmp_path / f"ckpt_{s}.pt").write_bytes(b"x")
+        (tmp_path / f"ckpt_{s}.pt.md5").write_text("0" * 32)
+    apply_retention(tmp_path, 2, distributed=False)
+    assert sorted(p.name for p in tmp_path.glob("*.pt")) == ["ckpt_10000.pt", "ckpt_2000.pt"]
+    assert not (tmp_path / "ckpt_300.pt.md5").exists()
+    d1, d2 = tmp_path / "ckpt_5", tmp_path / "ckpt_6"
+    d1.mkdir()
+    (d1 / ".metadata").write_bytes(b"m")
+    d2.mkdir()
+    (d2 / ".metadata").write_bytes(b"m")
+    (d2 / ".incomplete").write_text("")
+    assert get_latest_checkpoint(str(tmp_path), distributed=True) == str(d1)
+
+
+def _tiny_run(ckdir, steps, extra=()):
+    from pyrecover_amd.cli import get_args
+    from pyrecover_amd.trainer import train
+
+    return train(get_args(["--model-preset", "llama-micro", "--synthetic-data", "--sequence-length", "128",
+                           "--batch-size", "2", "--training-steps", str(steps), "--checkpoint-dir", str(ckdir),
+                           "--checkpoint-frequency", "2", "--model-dtype", "fp32", "--num-workers", "0"]
+                          + list(extra)))
+
+
+def test_weights_equality_tool(tmp_path):
+    sys.path.insert(0, str(ROOT / "tools"))
+    from check_weights_equality import main
+
+    _tiny_run(tmp_path / "a", 2)
+    _tiny_run(tmp_path / "b", 2)
+    _tiny_run(tmp_path / "c", 4)
+    a, b, c = (str(tmp_path / x / "default-exp" / "ckpt_2.pt") for x in "abc")
+    assert main([a, b, "--optimizer"]) == 0
+    assert main([a, str(tmp_path / "c" / "default-exp" / "ckpt_4.pt")]) == 1
+    assert main([a, str(tmp_path / "missing.pt")]) == 2
+    _tiny_run(tmp_path / "d", 2, ["--use-torch-distributed-ckpt"])
+    assert main([a, str(tmp_path / "d" / "default-exp" / "ckpt_2"), "--distributed"]) == 0
+
+
+def test_kill_during_save_never_corrupts_latest(tmp_path):
+    """A hard kill while ckpt_4 is being written leaves ckpt_2 as `latest` and loadable."""
+    code = ("import sys; sys.path.insert(0, %r); "
+            "from tests.test_framework import _tiny_run; _tiny_run(%r, 4, ['--verify-checkpoints'])"
+            % (str(ROOT), str(tmp_path)))
+    env = dict(os.environ, PYRECOVER_FAULT="kill_during_write:ckpt_4")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, timeout=300)
+    assert r.returncode == -9, r.stderr.decode()[-2000:]
+    from pyrecover_amd.ckpt.core import get_latest_checkpoint
+    from pyrecover_amd.ckpt.vanilla import verify_checkpoint
+
+    latest = get_latest_checkpoint(str(tmp_path / "default-exp"))
+    assert latest.endswith("ckpt_2.pt")
+    assert verify_checkpoint(latest)[0]
+    assert not (tmp_path / "default-exp" / "ckpt_4.pt").exists()
+    r = _tiny_run(tmp_path, 4, ["--resume-from-checkpoint", "latest", "--verify-checkpoints"])
+    assert r["step"] == 4
