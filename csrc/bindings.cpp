@@ -103,6 +103,63 @@ at::Tensor rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at::Tens
   return dx;
 }
 
+// LayerNorm: returns (h, y, mean, rstd)
+std::vector<at::Tensor> layernorm_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& delta, const at::Tensor& w,
+                                      const at::Tensor& b, double eps) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.is_contiguous() && w.is_contiguous() && b.is_contiguous(), "layernorm_fwd: contiguous");
+  const int64_t D = x.size(-1);
+  const int64_t rows = x.numel() / D;
+  TORCH_CHECK(w.numel() == D && b.numel() == D && w.scalar_type() == x.scalar_type() &&
+              b.scalar_type() == x.scalar_type(), "layernorm_fwd: weight/bias mismatch");
+  TORCH_CHECK(D % 8 == 0 && D <= 8192, "layernorm_fwd: D must be a multiple of 8 and <= 8192");
+  same_dev(x, w, "weight");
+  same_dev(x, b, "bias");
+  if (delta.has_value()) {
+    TORCH_CHECK(delta->sizes() == x.sizes() && delta->is_contiguous() && delta->scalar_type() == x.scalar_type(),
+                "layernorm_fwd: delta mismatch");
+    same_dev(x, *delta, "delta");
+  }
+  const c10::DeviceGuard guard(x.device());
+  at::Tensor y = at::empty_like(x);
+  auto fo = x.options().dtype(at::kFloat);
+  at::Tensor mean = at::empty({rows}, fo), rstd = at::empty({rows}, fo);
+  at::Tensor h = delta.has_value() ? at::empty_like(x) : x;
+  check(pra_layernorm_fwd(dt(x), x.data_ptr(), delta.has_value() ? delta->data_ptr() : nullptr, w.data_ptr(),
+                          b.data_ptr(), delta.has_value() ? h.data_ptr() : nullptr, y.data_ptr(), mean.data_ptr<float>(),
+                          rstd.data_ptr<float>(), (int)rows, (int)D, (float)eps, stream_of(x)),
+        "layernorm_fwd");
+  return {h, y, mean, rstd};
+}
+
+// dwb: 2*D contiguous output [dw | db]
+at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at::Tensor& w, const at::Tensor& mean,
+                         const at::Tensor& rstd, const c10::optional<at::Tensor>& dres, at::Tensor dwb, bool accumulate) {
+  check_dev(dy, "dy");
+  TORCH_CHECK(dy.is_contiguous() && h.is_contiguous() && dy.sizes() == h.sizes(), "layernorm_bwd: dy/h mismatch");
+  const int64_t D = h.size(-1);
+  const int64_t rows = h.numel() / D;
+  TORCH_CHECK(w.numel() == D && dwb.numel() == 2 * D && dwb.is_contiguous() && rstd.numel() == rows &&
+              mean.numel() == rows, "layernorm_bwd: shapes");
+  TORCH_CHECK(dwb.scalar_type() == h.scalar_type() && dy.scalar_type() == h.scalar_type() &&
+              rstd.scalar_type() == at::kFloat && mean.scalar_type() == at::kFloat, "layernorm_bwd: dtypes");
+  for (const at::Tensor& t : {h, w, mean, rstd, dwb}) same_dev(dy, t, "layernorm operand");
+  if (dres.has_value()) {
+    TORCH_CHECK(dres->sizes() == h.sizes() && dres->is_contiguous() && dres->scalar_type() == h.scalar_type(),
+                "layernorm_bwd: dres");
+    same_dev(dy, *dres, "dres");
+  }
+  const c10::DeviceGuard guard(h.device());
+  at::Tensor dx = at::empty_like(h);
+  const int wsr = pra_rmsnorm_bwd_ws_rows((int)rows);
+  at::Tensor ws = at::empty({wsr + 4, 2 * D}, h.options().dtype(at::kFloat));
+  check(pra_layernorm_bwd(dt(h), dy.data_ptr(), h.data_ptr(), w.data_ptr(), mean.data_ptr<float>(),
+                          rstd.data_ptr<float>(), dres.has_value() ? dres->data_ptr() : nullptr, dx.data_ptr(),
+                          dwb.data_ptr(), ws.data_ptr<float>(), (int)rows, (int)D, accumulate ? 1 : 0, stream_of(h)),
+        "layernorm_bwd");
+  return dx;
+}
+
 // In-place RoPE on the first `ncols` columns of each row of a 2-D [tokens, ld] buffer.
 void rope_(at::Tensor x2d, int64_t ncols, const at::Tensor& tab, int64_t head_dim, int64_t seq_len,
            int64_t pos_offset, bool inverse) {
@@ -331,6 +388,8 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "pyrecover_amd native ops (HIP/gfx950 kernels + checkpoint engine)";
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("layernorm_bwd", &layernorm_bwd);
   m.def("rope_", &rope_);
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);

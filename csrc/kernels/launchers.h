@@ -12,6 +12,12 @@ hipError_t pra_rmsnorm_bwd(int dtype, const void* dy, const void* h, const void*
                            const void* dres, void* dx, void* dw, float* ws, int rows, int D, int accumulate,
                            hipStream_t s);
 
+hipError_t pra_layernorm_fwd(int dtype, const void* x, const void* delta, const void* w, const void* b, void* h_out,
+                             void* y, float* mean, float* rstd, int rows, int D, float eps, hipStream_t s);
+hipError_t pra_layernorm_bwd(int dtype, const void* dy, const void* h, const void* w, const float* mean,
+                             const float* rstd, const void* dres, void* dx, void* dwb, float* ws, int rows, int D,
+                             int accumulate, hipStream_t s);
+
 hipError_t pra_rope(int dtype, void* x, const void* tab, long ntok, int ld, int ncols, int D, int S,
                     int pos_offset, int inverse, hipStream_t s);
 hipError_t pra_swiglu_fwd(int dtype, const void* g, const void* u, void* y, long ntok, int F, int ldg, int ldu,

@@ -160,6 +160,166 @@ __global__ __launch_bounds__(256) void colsum_stage2(const float* __restrict__ p
   out[c] = from_f<T>(s);
 }
 
+// ======================================================================================
+// LayerNorm (norm_type="layernorm", GPT-2-shape presets) with the same fused residual add.
+//   y = round((h - mean) * rstd * w + b)  (fp32 math, one rounding, like torch's layer_norm)
+// Backward: dxhat = dy*w; dx = rstd*(dxhat - mean(dxhat) - xhat*mean(dxhat*xhat)) (+ dres);
+// dw = sum(dy*xhat), db = sum(dy) -> partial rows [P][2D] reduced by the same colsum.
+template <typename T, int NV, bool HAS_DELTA>
+__global__ __launch_bounds__(256) void layernorm_fwd_kernel(
+    const T* __restrict__ x, const T* __restrict__ delta, const T* __restrict__ w, const T* __restrict__ bias,
+    T* __restrict__ h_out, T* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out, int rows,
+    int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const size_t base = (size_t)row * D;
+  float v[NV][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 8;
+    if (c < D) {
+      load8<T>(x + base + c, v[i]);
+      if constexpr (HAS_DELTA) {
+        float d[8];
+        load8<T>(delta + base + c, d);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] = rnd<T>(v[i][j] + d[j]);
+        store8<T>(h_out + base + c, v[i]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[i][j];
+    }
+  }
+  const float mean = wave_sum(s) / (float)D;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 8;
+    if (c < D) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float t = v[i][j] - mean;
+        ss += t * t;
+      }
+    }
+  }
+  const float r = rsqrtf(wave_sum(ss) / (float)D + eps);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 8;
+    if (c < D) {
+      float wv[8], bv[8], o[8];
+      load8<T>(w + c, wv);
+      load8<T>(bias + c, bv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mean) * r * wv[j] + bv[j];
+      store8<T>(y + base + c, o);
+    }
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = r;
+  }
+}
+
+template <typename T, int NVB, bool HAS_DRES>
+__global__ __launch_bounds__(256) void layernorm_bwd_kernel(
+    const T* __restrict__ dy, const T* __restrict__ h, const T* __restrict__ w, const float* __restrict__ mean_in,
+    const float* __restrict__ rstd, const T* dres, T* dx, float* __restrict__ part, int rows, int D) {
+  __shared__ float red[4];
+  const int tid = threadIdx.x;
+  float wv[NVB][8], dw[NVB][8], db[NVB][8];
+#pragma unroll
+  for (int i = 0; i < NVB; ++i) {
+    const int c = (i * 256 + tid) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { dw[i][j] = 0.f; db[i][j] = 0.f; }
+    if (c < D) load8<T>(w + c, wv[i]);
+  }
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    const size_t base = (size_t)row * D;
+    const float mu = mean_in[row], r = rstd[row];
+    float xh[NVB][8], g[NVB][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NVB; ++i) {
+      const int c = (i * 256 + tid) * 8;
+      if (c < D) {
+        float d[8];
+        load8<T>(h + base + c, xh[i]);
+        load8<T>(dy + base + c, d);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[i][j] = (xh[i][j] - mu) * r;
+          dw[i][j] += d[j] * xh[i][j];
+          db[i][j] += d[j];
+          g[i][j] = d[j] * wv[i][j];
+          s1 += g[i][j];
+          s2 += g[i][j] * xh[i][j];
+        }
+      }
+    }
+    s1 = block_sum<4>(s1, red) / (float)D;
+    s2 = block_sum<4>(s2, red) / (float)D;
+#pragma unroll
+    for (int i = 0; i < NVB; ++i) {
+      const int c = (i * 256 + tid) * 8;
+      if (c < D) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = rnd<T>(r * (g[i][j] - s1 - xh[i][j] * s2));
+        if constexpr (HAS_DRES) {
+          float d[8];
+          load8<T>(dres + base + c, d);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = o[j] + d[j];
+        }
+        store8<T>(dx + base + c, o);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NVB; ++i) {
+    const int c = (i * 256 + tid) * 8;
+    if (c < D) {
+      store8<float>(part + (size_t)blockIdx.x * 2 * D + c, dw[i]);
+      store8<float>(part + (size_t)blockIdx.x * 2 * D + D + c, db[i]);
+    }
+  }
+}
+
+template <typename T, int NV>
+static hipError_t ln_fwd_impl(const void* x, const void* delta, const void* w, const void* b, void* h_out, void* y,
+                              float* mean, float* rstd, int rows, int D, float eps, hipStream_t s) {
+  dim3 grid((rows + 3) / 4), block(256);
+  if (delta)
+    hipLaunchKernelGGL((layernorm_fwd_kernel<T, NV, true>), grid, block, 0, s, (const T*)x, (const T*)delta,
+                       (const T*)w, (const T*)b, (T*)h_out, (T*)y, mean, rstd, rows, D, eps);
+  else
+    hipLaunchKernelGGL((layernorm_fwd_kernel<T, NV, false>), grid, block, 0, s, (const T*)x, (const T*)nullptr,
+                       (const T*)w, (const T*)b, (T*)nullptr, (T*)y, mean, rstd, rows, D, eps);
+  return hipGetLastError();
+}
+
+template <typename T, int NVB>
+static hipError_t ln_bwd_impl(const void* dy, const void* h, const void* w, const float* mean, const float* rstd,
+                              const void* dres, void* dx, void* dwb, float* ws, int ws_rows, int rows, int D,
+                              int accumulate, hipStream_t s) {
+  if (dres)
+    hipLaunchKernelGGL((layernorm_bwd_kernel<T, NVB, true>), dim3(ws_rows), dim3(256), 0, s, (const T*)dy,
+                       (const T*)h, (const T*)w, mean, rstd, (const T*)dres, (T*)dx, ws, rows, D);
+  else
+    hipLaunchKernelGGL((layernorm_bwd_kernel<T, NVB, false>), dim3(ws_rows), dim3(256), 0, s, (const T*)dy,
+                       (const T*)h, (const T*)w, mean, rstd, (const T*)nullptr, (T*)dx, ws, rows, D);
+  const int D2 = 2 * D;
+  float* part2 = ws + (size_t)ws_rows * D2;
+  hipLaunchKernelGGL(colsum_stage1, dim3((D2 + 63) / 64, 4), dim3(256), 0, s, ws, part2, ws_rows, D2);
+  hipLaunchKernelGGL((colsum_stage2<T>), dim3((D2 + 255) / 256), dim3(256), 0, s, part2, (T*)dwb, D2, accumulate);
+  return hipGetLastError();
+}
+
 template <typename T, int NV>
 static hipError_t fwd_impl(const void* x, const void* delta, const void* w, void* h_out, void* y,
                            float* rstd, int rows, int D, float eps, hipStream_t s) {
@@ -218,6 +378,24 @@ hipError_t pra_rmsnorm_fwd(int dtype, const void* x, const void* delta, const vo
                            void* y, float* rstd, int rows, int D, float eps, hipStream_t s) {
   if (D % 8 != 0) return hipErrorInvalidValue;
   PRA_DISPATCH_FLOAT(dtype, T, PRA_NV_DISPATCH(D, NV, return pra::fwd_impl<T, NV>(x, delta, w, h_out, y, rstd, rows, D, eps, s)));
+  return hipSuccess;
+}
+
+// LayerNorm: dwb = [dw | db] (2*D contiguous, e.g. the flat gradient slot of weight|bias);
+// workspace = (pra_rmsnorm_bwd_ws_rows(rows) + 4) * 2 * D floats.
+hipError_t pra_layernorm_fwd(int dtype, const void* x, const void* delta, const void* w, const void* b, void* h_out,
+                             void* y, float* mean, float* rstd, int rows, int D, float eps, hipStream_t s) {
+  if (D % 8 != 0) return hipErrorInvalidValue;
+  PRA_DISPATCH_FLOAT(dtype, T, PRA_NV_DISPATCH(D, NV, return pra::ln_fwd_impl<T, NV>(x, delta, w, b, h_out, y, mean, rstd, rows, D, eps, s)));
+  return hipSuccess;
+}
+
+hipError_t pra_layernorm_bwd(int dtype, const void* dy, const void* h, const void* w, const float* mean,
+                             const float* rstd, const void* dres, void* dx, void* dwb, float* ws, int rows, int D,
+                             int accumulate, hipStream_t s) {
+  if (D % 8 != 0) return hipErrorInvalidValue;
+  const int ws_rows = pra_rmsnorm_bwd_ws_rows(rows);
+  PRA_DISPATCH_FLOAT(dtype, T, PRA_NVB_DISPATCH(D, NVB, return pra::ln_bwd_impl<T, NVB>(dy, h, w, mean, rstd, dres, dx, dwb, ws, ws_rows, rows, D, accumulate, s)));
   return hipSuccess;
 }
 

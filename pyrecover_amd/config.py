@@ -49,10 +49,12 @@ PRESETS = {
                                       multiple_of=1024, rope_theta=500000, vocab_size=131072),
     "llama2-7b": TransformerModelArgs(dim=4096, n_layers=32, n_heads=32, n_kv_heads=32, multiple_of=256,
                                       rope_theta=10000, vocab_size=32000),
+    # GPT-2 shapes (dims/heads/vocab padded to 50304) with LayerNorm; the block structure stays
+    # the reference's (RoPE, SwiGLU, untied head) -- "shape", as BASELINE.json configs 1-2 say.
     "gpt2-medium": TransformerModelArgs(dim=1024, n_layers=24, n_heads=16, n_kv_heads=16, multiple_of=256,
-                                        vocab_size=50304),
+                                        vocab_size=50304, norm_type="layernorm"),
     "gpt2-small": TransformerModelArgs(dim=768, n_layers=12, n_heads=12, n_kv_heads=12, multiple_of=256,
-                                       vocab_size=50304),
+                                       vocab_size=50304, norm_type="layernorm"),
     "llama-tiny": TransformerModelArgs(dim=256, n_layers=2, n_heads=4, n_kv_heads=2, multiple_of=64,
                                        vocab_size=512, rope_theta=10000),
     "llama-micro": TransformerModelArgs(dim=128, n_layers=2, n_heads=2, n_kv_heads=1, multiple_of=64,

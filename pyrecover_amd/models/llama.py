@@ -38,6 +38,27 @@ class RMSNorm(nn.Module):
         return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + self.eps)).type_as(x) * self.weight
 
 
+class LayerNorm(nn.Module):
+    """norm_type="layernorm" (the reference's TransformerModelArgs.norm_type field, model.py:18)."""
+
+    def __init__(self, dim: int, eps: float = 1e-5):
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(dim))
+        self.bias = nn.Parameter(torch.zeros(dim))
+
+    def forward(self, x):
+        return torch.nn.functional.layer_norm(x, (x.shape[-1],), self.weight, self.bias, self.eps)
+
+
+def make_norm(args: TransformerModelArgs, dim: int):
+    if args.norm_type == "rmsnorm":
+        return RMSNorm(dim, eps=args.norm_eps)
+    if args.norm_type == "layernorm":
+        return LayerNorm(dim, eps=args.norm_eps)
+    raise ValueError(f"unknown norm_type {args.norm_type!r}")
+
+
 class Attention(nn.Module):
     def __init__(self, args: TransformerModelArgs):
         super().__init__()
@@ -73,8 +94,8 @@ class TransformerBlock(nn.Module):
         self.feed_forward = FeedForward(args.dim, 4 * args.dim, args.multiple_of, args.ffn_dim_multiplier)
         self.layer_id = layer_id
         self.num_layers = args.n_layers
-        self.attention_norm = RMSNorm(args.dim, eps=args.norm_eps)
-        self.ffn_norm = RMSNorm(args.dim, eps=args.norm_eps)
+        self.attention_norm = make_norm(args, args.dim)
+        self.ffn_norm = make_norm(args, args.dim)
 
 
 class Transformer(nn.Module):
@@ -91,7 +112,7 @@ class Transformer(nn.Module):
         self.layers = nn.ModuleDict()
         for layer_id in range(model_args.n_layers):
             self.layers[str(layer_id)] = TransformerBlock(layer_id, model_args)
-        self.norm = RMSNorm(model_args.dim, eps=model_args.norm_eps)
+        self.norm = make_norm(model_args, model_args.dim)
         self.output = nn.Linear(model_args.dim, model_args.vocab_size, bias=False)
         self.register_buffer("rope_tab", rope_table(self.freqs_cis), persistent=False)
         self.flat: Optional[FlatParams] = None
@@ -120,18 +141,24 @@ class Transformer(nn.Module):
     def fusion_groups(self) -> List[List[Tuple[str, nn.Parameter]]]:
         """Flat-buffer layout in forward order (gradients become ready in reverse order, so DDP
         buckets are contiguous tail-first slices). Adjacent members form fused GEMM weights."""
+        def norm_group(prefix, mod):
+            grp = [(prefix + "weight", mod.weight)]
+            if getattr(mod, "bias", None) is not None:
+                grp.append((prefix + "bias", mod.bias))
+            return grp
+
         g = [[("tok_embeddings.weight", self.tok_embeddings.weight)]]
         for i, layer in self.layers.items():
             p = f"layers.{i}."
             at, ff = layer.attention, layer.feed_forward
-            g.append([(p + "attention_norm.weight", layer.attention_norm.weight)])
+            g.append(norm_group(p + "attention_norm.", layer.attention_norm))
             g.append([(p + "attention.wq.weight", at.wq.weight), (p + "attention.wk.weight", at.wk.weight),
                       (p + "attention.wv.weight", at.wv.weight)])
             g.append([(p + "attention.wo.weight", at.wo.weight)])
-            g.append([(p + "ffn_norm.weight", layer.ffn_norm.weight)])
+            g.append(norm_group(p + "ffn_norm.", layer.ffn_norm))
             g.append([(p + "feed_forward.w1.weight", ff.w1.weight), (p + "feed_forward.w3.weight", ff.w3.weight)])
             g.append([(p + "feed_forward.w2.weight", ff.w2.weight)])
-        g.append([("norm.weight", self.norm.weight)])
+        g.append(norm_group("norm.", self.norm))
         g.append([("output.weight", self.output.weight)])
         return g
 
@@ -155,6 +182,11 @@ class Transformer(nn.Module):
             return params[0].detach()
         return torch.cat([p.detach() for p in params], 0)
 
+    def _norm(self, mod, x, delta):
+        if isinstance(mod, LayerNorm):
+            return F.add_layer_norm(x, delta, mod.weight, mod.bias, self._slot([mod.weight, mod.bias]), mod.eps)
+        return F.add_rms_norm(x, delta, mod.weight, self._slot([mod.weight]), mod.eps)
+
     def _trunk(self, tokens: torch.Tensor):
         a = self.model_args
         B, S = tokens.shape
@@ -166,24 +198,21 @@ class Transformer(nn.Module):
         pending = None
         for layer in self.layers.values():
             at, ff = layer.attention, layer.feed_forward
-            wn1 = layer.attention_norm.weight
             if pending is None:
-                x, n1 = h, F.add_rms_norm(h, None, wn1, self._slot([wn1]), layer.attention_norm.eps)
+                x, n1 = h, self._norm(layer.attention_norm, h, None)
             else:
-                x, n1 = F.add_rms_norm(h, pending, wn1, self._slot([wn1]), layer.attention_norm.eps)
+                x, n1 = self._norm(layer.attention_norm, h, pending)
             qkv_p = [at.wq.weight, at.wk.weight, at.wv.weight]
             att = F.attention_block(n1, self._weight(qkv_p), self._weight([at.wo.weight]), self._slot(qkv_p),
                                     self._slot([at.wo.weight]), self.rope_tab, dims, qkv_p + [at.wo.weight])
-            wn2 = layer.ffn_norm.weight
-            x2, n2 = F.add_rms_norm(x, att, wn2, self._slot([wn2]), layer.ffn_norm.eps)
+            x2, n2 = self._norm(layer.ffn_norm, x, att)
             up = [ff.w1.weight, ff.w3.weight]
             mlp = F.swiglu_mlp(n2, self._weight(up), self._weight([ff.w2.weight]), self._slot(up),
                                self._slot([ff.w2.weight]), up + [ff.w2.weight])
             h, pending = x2, mlp
-        wn = self.norm.weight
         if pending is None:
-            return F.add_rms_norm(h, None, wn, self._slot([wn]), self.norm.eps)
-        _, nf = F.add_rms_norm(h, pending, wn, self._slot([wn]), self.norm.eps)
+            return self._norm(self.norm, h, None)
+        _, nf = self._norm(self.norm, h, pending)
         return nf
 
     def forward(self, tokens: torch.Tensor, labels: Optional[torch.Tensor] = None, ignore_index: int = -100):

@@ -2,6 +2,7 @@
 from .fused import (  # noqa: F401
     FlatSlotAdapter,
     UnflatSlot,
+    add_layer_norm,
     add_rms_norm,
     attention_block,
     embedding,

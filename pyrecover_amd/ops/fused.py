@@ -155,6 +155,61 @@ def add_rms_norm(x, delta, weight, slot, eps):
 
 
 # ---------------------------------------------------------------------------------------
+class _AddLayerNorm(torch.autograd.Function):
+    """LayerNorm variant (norm_type="layernorm"): (h, y) = (x + delta, layer_norm(x + delta)*w + b).
+    Gradients of weight|bias land in one slot (the two params are adjacent in the flat buffer)."""
+
+    @staticmethod
+    def forward(ctx, x, delta, weight, bias, slot, eps):
+        ctx.slot = slot
+        ctx.has_delta = delta is not None
+        ctx.eps = eps
+        if x.is_cuda:
+            h, y, mean, rstd = _ext.require_for(x).layernorm_fwd(
+                x.contiguous(), delta.contiguous() if delta is not None else None, weight, bias, eps)
+        else:
+            h = x if delta is None else x + delta
+            y = torch.nn.functional.layer_norm(h, (h.shape[-1],), weight, bias, eps)
+            mean = rstd = torch.empty(0)
+        ctx.save_for_backward(h, weight, bias, mean, rstd)
+        if delta is None:
+            return y
+        return h, y
+
+    @staticmethod
+    def backward(ctx, *grads):
+        h, weight, bias, mean, rstd = ctx.saved_tensors
+        dh, dy = grads if ctx.has_delta else (None, grads[0])
+        slot = ctx.slot
+        buf, acc = slot.begin(dy)
+        D = h.shape[-1]
+        if dy.is_cuda:
+            dx = _ext.require_for(dy).layernorm_bwd(dy.contiguous(), h, weight, mean, rstd,
+                                                    dh.contiguous() if dh is not None else None, buf, acc)
+        else:
+            with torch.enable_grad():
+                hh = h.detach().requires_grad_()
+                ww = weight.detach().requires_grad_()
+                bb = bias.detach().requires_grad_()
+                yy = torch.nn.functional.layer_norm(hh, (D,), ww, bb, ctx.eps)
+                gx, gw, gb = torch.autograd.grad(yy, (hh, ww, bb), dy)
+            dx = gx if dh is None else gx + dh
+            g = torch.cat([gw.reshape(-1), gb.reshape(-1)]).to(buf.dtype)
+            if acc:
+                buf.add_(g)
+            else:
+                buf.copy_(g)
+        slot.end(buf)
+        if ctx.has_delta:
+            return dx, dx, None, None, None, None
+        return dx, None, None, None, None, None
+
+
+def add_layer_norm(x, delta, weight, bias, slot, eps):
+    return _AddLayerNorm.apply(x, delta, weight, bias, slot, eps)
+
+
+# ---------------------------------------------------------------------------------------
 def _attn_fwd(q, k, v, scale, causal):
     if q.is_cuda:
         return _ext.require_for(q).attn_fwd(q, k, v, scale, causal)

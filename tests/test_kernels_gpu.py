@@ -48,6 +48,32 @@ def test_rmsnorm(cuda, rows, D, with_delta):
     assert _rel(dw2, 2 * dw.float()) < 1e-2
 
 
+@pytest.mark.parametrize("rows,D", [(333, 1024), (64, 768)])
+@pytest.mark.parametrize("with_delta", [False, True])
+def test_layernorm(cuda, rows, D, with_delta):
+    C = _ext.native()
+    torch.manual_seed(0)
+    x = torch.randn(rows, D, device=cuda, dtype=torch.bfloat16)
+    d = torch.randn(rows, D, device=cuda, dtype=torch.bfloat16) if with_delta else None
+    w = (1 + 0.1 * torch.randn(D, device=cuda)).bfloat16()
+    b = (0.1 * torch.randn(D, device=cuda)).bfloat16()
+    h, y, mean, rstd = C.layernorm_fwd(x, d, w, b, 1e-5)
+    h_ref = x if d is None else x + d
+    hf = h_ref.float().requires_grad_()
+    wf, bf = w.float().requires_grad_(), b.float().requires_grad_()
+    yf = torch.nn.functional.layer_norm(hf, (D,), wf, bf, 1e-5)
+    assert torch.equal(h, h_ref)
+    assert _rel(y, yf) < 1e-2
+    dy = torch.randn_like(x)
+    dres = torch.randn_like(x) if with_delta else None
+    yf.backward(dy.float())
+    dwb = torch.empty(2 * D, device=cuda, dtype=torch.bfloat16)
+    dx = C.layernorm_bwd(dy, h, w, mean, rstd, dres, dwb, False)
+    gx = hf.grad + (dres.float() if dres is not None else 0)
+    assert _rel(dx, gx) < 2e-2
+    assert _rel(dwb[:D], wf.grad) < 2e-2 and _rel(dwb[D:], bf.grad) < 2e-2
+
+
 def test_rope(cuda):
     C = _ext.native()
     B, S, Hq, Hkv, D = 2, 256, 4, 2, 128

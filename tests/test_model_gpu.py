@@ -14,24 +14,25 @@ def ref_forward(m, tok):
     h = torch.nn.functional.embedding(tok, m.tok_embeddings.weight)
     for L in m.layers.values():
         at = L.attention
-        x = R.rmsnorm_ref(h, L.attention_norm.weight, L.attention_norm.eps)
+        x = L.attention_norm(h)
         q = (x @ at.wq.weight.t()).view(B, S, at.n_heads, at.head_dim)
         k = (x @ at.wk.weight.t()).view(B, S, at.n_kv_heads, at.head_dim)
         v = (x @ at.wv.weight.t()).view(B, S, at.n_kv_heads, at.head_dim)
         q, k = R.apply_rotary_emb_ref(q, k, m.freqs_cis)
         o = R.attention_ref(q, k, v, True).reshape(B, S, -1)
         h = h + o @ at.wo.weight.t()
-        x = R.rmsnorm_ref(h, L.ffn_norm.weight, L.ffn_norm.eps)
+        x = L.ffn_norm(h)
         ff = L.feed_forward
         h = h + R.swiglu_ref(x @ ff.w1.weight.t(), x @ ff.w3.weight.t()) @ ff.w2.weight.t()
-    h = R.rmsnorm_ref(h, m.norm.weight, m.norm.eps)
+    h = m.norm(h)
     return h @ m.output.weight.t()
 
 
-@pytest.mark.parametrize("preset", ["llama-micro", "llama-tiny"])
-def test_model_grads_vs_fp32_reference(cuda, preset):
+@pytest.mark.parametrize("preset,over", [("llama-micro", {}), ("llama-tiny", {}),
+                                         ("gpt2-small", {"n_layers": 2, "vocab_size": 1024})])
+def test_model_grads_vs_fp32_reference(cuda, preset, over):
     torch.manual_seed(0)
-    a = get_preset(preset, seq_len=256)
+    a = get_preset(preset, seq_len=256, **over)
     cpu = Transformer(a)
     B, S = 2, 256
     tok = torch.randint(0, a.vocab_size, (B, S))

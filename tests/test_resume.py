@@ -115,3 +115,36 @@ def test_corrupted_checkpoint_is_refused(tmp_path):
     p.write_bytes(bytes(data))
     with pytest.raises(RuntimeError, match="Checksum mismatch"):
         train(_args(tmp_path, 6, resume="latest"))
+
+
+def test_baseline_config1_gpt2_small_fp32_cpu(tmp_path):
+    """BASELINE.json config 1: GPT-2-small-shape fp32, seq 128, world_size 1 on CPU, save + resume
+    through the pyrecover.checkpoint API (reference-compatible package)."""
+    import pyrecover
+    from pyrecover_amd.config import get_preset
+    from pyrecover_amd.models.llama import Transformer
+    from pyrecover_amd.optim.adamw import FlatAdamW
+    from pyrecover_amd.optim.lr import build_lr_scheduler
+
+    def build():
+        torch.manual_seed(0)
+        m = Transformer(get_preset("gpt2-small", seq_len=128))
+        flat = m.flatten_()
+        o = FlatAdamW(flat, lr=1e-3)
+        return m, o, build_lr_scheduler(o, 10)
+
+    tok = torch.randint(0, 50304, (2, 129), generator=torch.Generator().manual_seed(1))
+    m, o, s = build()
+    for _ in range(2):
+        o.zero_grad()
+        m(tok[:, :-1], labels=tok[:, 1:]).backward()
+        o.step()
+        s.step()
+    p = str(tmp_path / "ckpt_2.pt")
+    pyrecover.save_ckpt_vanilla(m, o, s, None, 2, 1, p, max_keep=3, verify=True)
+    m2, o2, s2 = build()
+    epoch, step = pyrecover.load_ckpt_vanilla(m2, o2, s2, None, "latest", experiment_dir=str(tmp_path), verify=True)
+    assert (epoch, step) == (1, 2)
+    for (k, a), (_, b) in zip(m.state_dict().items(), m2.state_dict().items()):
+        assert torch.equal(a, b), k
+    assert torch.equal(o.exp_avg_sq, o2.exp_avg_sq) and s.state_dict() == s2.state_dict()
