@@ -19,6 +19,8 @@
 //    over key tiles). P is recomputed from the saved log-sum-exp.
 #include "common.h"
 
+#include <type_traits>
+
 namespace pra {
 namespace attn {
 
@@ -100,8 +102,72 @@ struct Stage {
   }
 };
 
+// LDS-DMA staging (global_load_lds_dwordx4) of a ROWS x D tile into the swizzled image. The DMA
+// writes 1 KiB per wave-instruction linearly (base + 16 B * lane), so each lane fetches the
+// logical chunk that the swizzle places at its linear position (the XOR swizzle is an involution).
+// No VGPR staging; rows must be in bounds (callers guarantee S % tile == 0).
+template <int D, int ROWS>
+struct GStage {
+  static constexpr int CH = D / 8;
+  static constexpr int NI = ROWS * CH / 256;
+  int off[NI];  // element offset of this lane's source chunk relative to the tile's first row
+  __device__ __forceinline__ void init(long ld) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int idx = (i * 4 + wid) * 64 + lane;
+      const int row = idx / CH, pc = idx % CH;
+      off[i] = row * (int)ld + swz<D>(row, pc) * 8;
+    }
+  }
+  __device__ __forceinline__ void issue(const __bf16* g, __bf16* tile) const {
+    const int wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(g + off[i]),
+                                       (__attribute__((address_space(3))) void*)(tile + (i * 4 + wid) * 512), 16, 0,
+                                       0);
+  }
+};
+
 // C-layout row of register r for lane half h (32x32 accumulator)
 __device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// Lane-invariant LDS offsets (in elements) for the fragment reads of a swizzled [rows][D] tile.
+// Valid for any row base that is a multiple of 16 (the swizzle only depends on row & 15), so the
+// per-tile part of every address is a compile-time constant folded into the ds_read immediate.
+template <int D>
+struct LaneOff {
+  static constexpr int NKS = D / 16, NDB = D / 32;
+  int row[NKS];            // ds_read_b128 of row (base + l32), chunk 2*ks + h2
+  int trl[NDB], trh[NDB];  // ds_read_b64_tr_b16 blocks of tr_frag(r0 = base, c0 = db*32)
+  __device__ __forceinline__ void init(int lane) {
+    const int l32 = lane & 31, h2 = lane >> 5;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) row[ks] = lds_off<D>(l32, 2 * ks + h2);
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int r = 4 * (g >> 1) + q;
+#pragma unroll
+    for (int db = 0; db < NDB; ++db) {
+      const int col = db * 32 + 16 * (g & 1) + 4 * p;
+      trl[db] = lds_off<D>(r, col >> 3) + (col & 7);
+      trh[db] = lds_off<D>(r + 8, col >> 3) + (col & 7);
+    }
+  }
+  // transposed 32x16 operand block of rows [r0, r0+16) (r0 % 16 == 0), cols [db*32, db*32+32)
+  __device__ __forceinline__ bf16x8 tr(const __bf16* tile, int r0, int db) const {
+    const i16x4 lo = tr4(tile + r0 * D + trl[db]);
+    const i16x4 hi = tr4(tile + r0 * D + trh[db]);
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  }
+  // row operand: rows [r0, r0+32) (r0 % 16 == 0), k-step ks
+  __device__ __forceinline__ bf16x8 rowk(const __bf16* tile, int r0, int ks) const {
+    return lds_row8(tile, r0 * D + row[ks]);
+  }
+};
+
+template <int N>
+using IC = std::integral_constant<int, N>;
 
 // ======================================================================================
 // Forward
@@ -112,8 +178,8 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const __bf16* __restrict__ 
                                                      float* __restrict__ LSE, int S, int Hq, int Hkv, long ldq,
                                                      long ldk, long ldv, long ldo, float scale_log2) {
   constexpr int KT = 64, QT = 128;
-  constexpr int NKS = D / 16, NDB = D / 32;
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2][2][KT * D];
+  constexpr int NKS = D / 16, NDB = D / 32, TILE = KT * D;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[4 * TILE];  // K0 V0 K1 V1
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h2 = lane >> 5, l32 = lane & 31;
   const int nqt = (S + QT - 1) / QT;
@@ -128,21 +194,18 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const __bf16* __restrict__ 
   const __bf16* Kb = K + (long)b * S * ldk + hk * D;
   const __bf16* Vb = V + (long)b * S * ldv + hk * D;
 
-  // Q fragments (B operand of S^T = K Q^T): lane holds Q[qw + l32][16 ks + 8 h2 .. +7]
-  bf16x8 qf[NKS];
+  LaneOff<D> lo;
+  lo.init(lane);
+  bf16x8 qf[NKS];  // B operand of S^T = K Q^T: lane holds Q[qw + l32][16 ks + 8 h2 .. +7]
   const int qrow = qw + l32;
 #pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) {
-    if (qrow < S)
-      qf[ks] = *reinterpret_cast<const bf16x8*>(Qb + (long)qrow * ldq + 16 * ks + 8 * h2);
-    else
-      qf[ks] = bf16x8{};
-  }
+  for (int ks = 0; ks < NKS; ++ks)
+    qf[ks] = qrow < S ? *reinterpret_cast<const bf16x8*>(Qb + (long)qrow * ldq + 16 * ks + 8 * h2) : bf16x8{};
 
   f32x16 o[NDB];
 #pragma unroll
   for (int i = 0; i < NDB; ++i) o[i] = f32x16{};
-  float m_i = -INFINITY, l_i = 0.f;
+  float m_i = -INFINITY, l_i = 0.f;  // running max (log2 units of scaled scores) and sum
 
   const int kend = CAUSAL ? min(S, q0 + QT) : S;
   const int nkt = (kend + KT - 1) / KT;
@@ -150,79 +213,86 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const __bf16* __restrict__ 
   Stage<D, KT> sk, sv;
   sk.load(Kb, ldk, 0, S);
   sv.load(Vb, ldv, 0, S);
-  sk.store(smem[0][0]);
-  sv.store(smem[0][1]);
+  sk.store(smem);
+  sv.store(smem + TILE);
   __syncthreads();
 
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int cur = kt & 1;
+  auto body = [&](auto cc, int kt) {
+    constexpr int CUR = decltype(cc)::value;
+    const __bf16* Kt = smem + 2 * CUR * TILE;
+    const __bf16* Vt = Kt + TILE;
     const int k0 = kt * KT;
-    if (kt + 1 < nkt) {
+    const bool more = kt + 1 < nkt;
+    if (more) {  // issue-early / write-late staging of the next K/V tile (T14)
       sk.load(Kb, ldk, k0 + KT, S);
       sv.load(Vb, ldv, k0 + KT, S);
     }
     if (!(CAUSAL && k0 > qw + 31)) {
-      const __bf16* kt_lds = smem[cur][0];
-      const __bf16* vt_lds = smem[cur][1];
-      f32x16 s[2];
+      // S^T = K Q^T, two 32-key halves, next fragments issued before the current MFMAs
+      f32x16 s0 = f32x16{}, s1 = f32x16{};
+      bf16x8 a0 = lo.rowk(Kt, 0, 0), a1 = lo.rowk(Kt, 32, 0);
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-        s[kb] = f32x16{};
+      for (int ks = 0; ks < NKS; ++ks) {
+        bf16x8 n0 = a0, n1 = a1;
+        if (ks + 1 < NKS) {
+          n0 = lo.rowk(Kt, 0, ks + 1);
+          n1 = lo.rowk(Kt, 32, ks + 1);
+        }
+        s0 = mfma(a0, qf[ks], s0);
+        s1 = mfma(a1, qf[ks], s1);
+        a0 = n0;
+        a1 = n1;
+      }
+      if (CAUSAL && k0 + KT - 1 > qw) {  // diagonal tile: mask keys beyond the query
 #pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-          const bf16x8 kf = lds_row8(kt_lds, lds_off<D>(kb * 32 + l32, 2 * ks + h2));
-          s[kb] = mfma(kf, qf[ks], s[kb]);
+        for (int r = 0; r < 16; ++r) {
+          if (k0 + crow(r, h2) > qrow) s0[r] = -INFINITY;
+          if (k0 + 32 + crow(r, h2) > qrow) s1[r] = -INFINITY;
         }
       }
-      // online softmax in the log2 domain; query = qw + l32 is lane-local
       float mx = -INFINITY;
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, fmaxf(s0[r], s1[r]));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * scale_log2;
+      // exact deferred rescale: only when some row's running max grows in this wave
+      if (!__all(mx <= m_i)) {
+        const float m_new = fmaxf(m_i, mx);
+        const float alpha = fexp2(m_i - m_new);
+        l_i *= alpha;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float v = s[kb][r] * scale_log2;
-          if constexpr (CAUSAL) {
-            const int key = k0 + kb * 32 + crow(r, h2);
-            if (key > qrow) v = -INFINITY;
-          }
-          s[kb][r] = v;
-          mx = fmaxf(mx, v);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m_i, mx);
-      const float alpha = fexp2(m_i - m_new);
+        for (int i = 0; i < NDB; ++i) o[i] *= alpha;
+        m_i = m_new;
+      }
       float rs = 0.f;
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+      for (int r = 0; r < 16; ++r) {
+        s0[r] = fexp2(fmaf(s0[r], scale_log2, -m_i));
+        s1[r] = fexp2(fmaf(s1[r], scale_log2, -m_i));
+        rs += s0[r] + s1[r];
+      }
+      l_i += rs + __shfl_xor(rs, 32, 64);
+      const bf16x8 p00 = pack8(s0, 0), p01 = pack8(s0, 1), p10 = pack8(s1, 0), p11 = pack8(s1, 1);
+      // O^T[d][q] += V^T[d][key] P^T[key][q]; V^T fragments prefetched one MFMA ahead
+      bf16x8 vc = lo.tr(Vt, 0, 0);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = fexp2(s[kb][r] - m_new);
-          s[kb][r] = p;
-          rs += p;
-        }
-      rs += __shfl_xor(rs, 32, 64);
-      l_i = l_i * alpha + rs;
-      m_i = m_new;
-#pragma unroll
-      for (int i = 0; i < NDB; ++i) o[i] *= alpha;
-      // O^T[d][q] += V^T[d][key] * P^T[key][q]
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const bf16x8 pf = pack8(s[kb], s2);
-#pragma unroll
-          for (int db = 0; db < NDB; ++db) {
-            const bf16x8 vf = tr_frag<D>(vt_lds, kb * 32 + 16 * s2, db * 32, lane);
-            o[db] = mfma(vf, pf, o[db]);
-          }
-        }
+      for (int st = 0; st < 4 * NDB; ++st) {
+        const int k4 = st / NDB, db = st % NDB;
+        bf16x8 vn = vc;
+        if (st + 1 < 4 * NDB) vn = lo.tr(Vt, ((st + 1) / NDB) * 16, (st + 1) % NDB);
+        const bf16x8 pf = k4 == 0 ? p00 : k4 == 1 ? p01 : k4 == 2 ? p10 : p11;
+        o[db] = mfma(vc, pf, o[db]);
+        vc = vn;
+      }
     }
-    if (kt + 1 < nkt) {
-      sk.store(smem[cur ^ 1][0]);
-      sv.store(smem[cur ^ 1][1]);
+    if (more) {
+      sk.store(smem + 2 * (1 - CUR) * TILE);
+      sv.store(smem + 2 * (1 - CUR) * TILE + TILE);
     }
     __syncthreads();
+  };
+  for (int kt = 0; kt < nkt; kt += 2) {
+    body(IC<0>{}, kt);
+    if (kt + 1 < nkt) body(IC<1>{}, kt + 1);
   }
 
   if (qrow < S) {
@@ -274,22 +344,29 @@ __global__ __launch_bounds__(256) void bwd_pre_kernel(const __bf16* __restrict__
 }
 
 // ======================================================================================
-// Backward dK/dV: block = (b, kv head, 128-key tile); wave owns 32 keys in registers.
-// Loops over the query heads of the kv head and over 32-row query tiles.
-//   S  = Q K^T   (key on lane)      P  = exp2(S*c - lse2)
+// Backward dK/dV: block = (b, kv head, 128-key tile); wave owns 32 keys. K and V of the block
+// stay resident in LDS (read as MFMA operands, so only the dK/dV accumulators live in registers
+// and the kernel fits 2 waves/SIMD); 32-row Q/dO tiles stream through a single LDS buffer,
+// register-staged one tile ahead. Loops over the query heads of the kv head (GQA) and query tiles.
+//   S  = Q K^T   (key on lane)      P  = exp2(S*c - lse*log2e)
 //   dP = dO V^T  (key on lane)      dS = P * (dP - delta)
 //   dV^T += dO^T P                  dK^T += Q^T dS      (accumulators reused as B operands)
+// Per-query constants arrive as one float per lane and are broadcast with ds_bpermute.
 // ======================================================================================
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(
+__global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(
     const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ V,
     const __bf16* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
     __bf16* __restrict__ dK, __bf16* __restrict__ dV, int S, int Hq, int Hkv, long ldq, long ldk, long ldv,
     long lddo, long lddk, long lddv, float scale, float scale_log2) {
   constexpr int KB = 128, QT = 32;
   constexpr int NKS = D / 16, NDB = D / 32;
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2][2][QT * D];  // [buf][Q/dO]
-  __shared__ __attribute__((aligned(16))) float rowc[2][2][QT];        // [buf][lse*/delta]
+  constexpr int KVT = KB * D, QDT = QT * D;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * KVT + 2 * QDT];  // K V Q dO
+  __bf16* const Ks = smem;
+  __bf16* const Vs = smem + KVT;
+  __bf16* const Qs = smem + 2 * KVT;
+  __bf16* const Ds = smem + 2 * KVT + QDT;
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h2 = lane >> 5, l32 = lane & 31;
   const int nkb = S / KB;
@@ -301,17 +378,18 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(
   const int k0 = kbk * KB, kw = k0 + wid * 32;
   const int krow = kw + l32;
 
-  // K/V fragments as B operands: lane holds K[krow][16 ks + 8 h2 .. +7]
-  bf16x8 kf[NKS], vf[NKS];
   {
-    const __bf16* Kr = K + ((long)b * S + krow) * ldk + hk * D + 8 * h2;
-    const __bf16* Vr = V + ((long)b * S + krow) * ldv + hk * D + 8 * h2;
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-      kf[ks] = *reinterpret_cast<const bf16x8*>(Kr + 16 * ks);
-      vf[ks] = *reinterpret_cast<const bf16x8*>(Vr + 16 * ks);
-    }
+    GStage<D, KB> gk, gv;
+    gk.init(ldk);
+    gv.init(ldv);
+    gk.issue(K + ((long)b * S + k0) * ldk + hk * D, Ks);
+    gv.issue(V + ((long)b * S + k0) * ldv + hk * D, Vs);
   }
+  const __bf16* Kw = Ks + wid * 32 * D;
+  const __bf16* Vw = Vs + wid * 32 * D;
+  LaneOff<D> lo;
+  lo.init(lane);
+
   f32x16 dkt[NDB], dvt[NDB];
 #pragma unroll
   for (int i = 0; i < NDB; ++i) { dkt[i] = f32x16{}; dvt[i] = f32x16{}; }
@@ -319,7 +397,10 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(
   const int qstart = CAUSAL ? k0 : 0;
   const int nqt = (S - qstart) / QT;
   const int total = nqt * nrep;
-  const float inv_c = 1.f / scale_log2;
+  // lane reads the row constant of query row l32 of the tile: lse*log2e (h2 = 0) or delta (h2 = 1)
+  const float rc_mul = h2 ? 1.f : 1.4426950408889634f;
+  const float* rc_base = (h2 ? Delta : LSE) + (long)b * Hq * S + l32;
+  const int bp_base = 4 * (4 * h2);  // ds_bpermute byte address of lane crow(0, h2)
 
   Stage<D, QT> sq, sd;
   auto stage_load = [&](int it) {
@@ -328,72 +409,58 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(
     sq.load(Q + (long)b * S * ldq + hq * D, ldq, q0, S);
     sd.load(dO + (long)b * S * lddo + hq * D, lddo, q0, S);
   };
-  auto stage_rows = [&](int it, int buf) {
-    const int hq = hk * nrep + it / nqt;
-    const int q0 = qstart + (it % nqt) * QT;
-    if (threadIdx.x < QT)
-      rowc[buf][0][threadIdx.x] = -LSE[((long)b * Hq + hq) * S + q0 + threadIdx.x] * 1.4426950408889634f * inv_c;
-    else if (threadIdx.x < 2 * QT)
-      rowc[buf][1][threadIdx.x - QT] = -Delta[((long)b * Hq + hq) * S + q0 + threadIdx.x - QT];
-  };
-
-  if (total > 0) {
-    stage_load(0);
-    sq.store(smem[0][0]);
-    sd.store(smem[0][1]);
-    stage_rows(0, 0);
-  }
-  __syncthreads();
+  if (total > 0) stage_load(0);
 
   for (int it = 0; it < total; ++it) {
-    const int cur = it & 1;
+    const int hq = hk * nrep + it / nqt;
     const int q0 = qstart + (it % nqt) * QT;
+    sq.store(Qs);
+    sd.store(Ds);
+    const float rcv = rc_base[(long)hq * S + q0] * rc_mul;
+    __syncthreads();
     if (it + 1 < total) stage_load(it + 1);
     if (!(CAUSAL && q0 + QT - 1 < kw)) {
-      const __bf16* qt_lds = smem[cur][0];
-      const __bf16* dt_lds = smem[cur][1];
-      f32x16 s, dp;
-      // row constants as the initial accumulators (rows = queries crow(r,h2))
+      f32x16 s = f32x16{}, dp = f32x16{};
+      // S chain then dP chain: one operand pair in flight ahead of each MFMA
+      bf16x8 xa = lo.rowk(Qs, 0, 0), xb = lo.rowk(Kw, 0, 0);
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const float4 a = *reinterpret_cast<const float4*>(&rowc[cur][0][8 * rr + 4 * h2]);
-        const float4 c = *reinterpret_cast<const float4*>(&rowc[cur][1][8 * rr + 4 * h2]);
-        s[4 * rr + 0] = a.x; s[4 * rr + 1] = a.y; s[4 * rr + 2] = a.z; s[4 * rr + 3] = a.w;
-        dp[4 * rr + 0] = c.x; dp[4 * rr + 1] = c.y; dp[4 * rr + 2] = c.z; dp[4 * rr + 3] = c.w;
+      for (int st = 0; st < 2 * NKS; ++st) {
+        const int ks = st % NKS;
+        bf16x8 na = xa, nb = xb;
+        if (st + 1 < 2 * NKS) {
+          const int nks = (st + 1) % NKS;
+          na = lo.rowk(st + 1 < NKS ? Qs : Ds, 0, nks);
+          nb = lo.rowk(st + 1 < NKS ? Kw : Vw, 0, nks);
+        }
+        if (st < NKS) s = mfma(xa, xb, s);
+        else dp = mfma(xa, xb, dp);
+        xa = na; xb = nb;
       }
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        const bf16x8 qa = lds_row8(qt_lds, lds_off<D>(l32, 2 * ks + h2));
-        s = mfma(qa, kf[ks], s);
-        const bf16x8 da = lds_row8(dt_lds, lds_off<D>(l32, 2 * ks + h2));
-        dp = mfma(da, vf[ks], dp);
-      }
+      const bool diag = CAUSAL && q0 == kw;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float p = fexp2(s[r] * scale_log2);
-        if constexpr (CAUSAL) {
-          if (krow > q0 + crow(r, h2)) p = 0.f;
-        }
+        const int src = bp_base + 4 * ((r & 3) + 8 * (r >> 2));
+        const float lse2 = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(rcv)));
+        const float dl = __int_as_float(__builtin_amdgcn_ds_bpermute(src + 128, __float_as_int(rcv)));
+        float p = fexp2(fmaf(s[r], scale_log2, -lse2));
+        if (diag && l32 > crow(r, h2)) p = 0.f;
         s[r] = p;
-        dp[r] = p * dp[r];
+        dp[r] = p * (dp[r] - dl);
       }
+      const bf16x8 p0 = pack8(s, 0), p1 = pack8(s, 1), d0 = pack8(dp, 0), d1 = pack8(dp, 1);
+      bf16x8 ot = lo.tr(Ds, 0, 0), qt = lo.tr(Qs, 0, 0);
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 pf = pack8(s, s2);
-        const bf16x8 df = pack8(dp, s2);
-#pragma unroll
-        for (int db = 0; db < NDB; ++db) {
-          const bf16x8 doT = tr_frag<D>(dt_lds, 16 * s2, db * 32, lane);
-          dvt[db] = mfma(doT, pf, dvt[db]);
-          const bf16x8 qT = tr_frag<D>(qt_lds, 16 * s2, db * 32, lane);
-          dkt[db] = mfma(qT, df, dkt[db]);
+      for (int st = 0; st < 2 * NDB; ++st) {
+        const int s2 = st / NDB, db = st % NDB;
+        bf16x8 no = ot, nq = qt;
+        if (st + 1 < 2 * NDB) {
+          no = lo.tr(Ds, 16 * ((st + 1) / NDB), (st + 1) % NDB);
+          nq = lo.tr(Qs, 16 * ((st + 1) / NDB), (st + 1) % NDB);
         }
+        dvt[db] = mfma(ot, s2 ? p1 : p0, dvt[db]);
+        dkt[db] = mfma(qt, s2 ? d1 : d0, dkt[db]);
+        ot = no; qt = nq;
       }
-    }
-    if (it + 1 < total) {
-      sq.store(smem[cur ^ 1][0]);
-      sd.store(smem[cur ^ 1][1]);
-      stage_rows(it + 1, cur ^ 1);
     }
     __syncthreads();
   }
@@ -416,19 +483,20 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(
 }
 
 // ======================================================================================
-// Backward dQ: block = (b, q head, 128 query rows), wave owns 32 queries; loop over key tiles.
+// Backward dQ: block = (b, q head, 128 query rows), wave owns 32 queries; loop over 64-key tiles
+// (double-buffered in LDS, staged issue-early / write-late).
 //   S^T = K Q^T, dP^T = V dO^T (query on lane; lse/delta are lane constants)
 //   dQ^T += K^T dS^T
 // ======================================================================================
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, 1) void bwd_dq_kernel(
+__global__ __launch_bounds__(256, 2) void bwd_dq_kernel(
     const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ V,
     const __bf16* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
     __bf16* __restrict__ dQ, int S, int Hq, int Hkv, long ldq, long ldk, long ldv, long lddo, long lddq,
     float scale, float scale_log2) {
   constexpr int KT = 64, QT = 128;
-  constexpr int NKS = D / 16, NDB = D / 32;
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2][2][KT * D];
+  constexpr int NKS = D / 16, NDB = D / 32, TILE = KT * D;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[4 * TILE];  // K0 V0 K1 V1
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h2 = lane >> 5, l32 = lane & 31;
   const int nqt = (S + QT - 1) / QT;
@@ -443,6 +511,8 @@ __global__ __launch_bounds__(256, 1) void bwd_dq_kernel(
   const __bf16* Kb = K + (long)b * S * ldk + hk * D;
   const __bf16* Vb = V + (long)b * S * ldv + hk * D;
 
+  LaneOff<D> lo;
+  lo.init(lane);
   bf16x8 qf[NKS], df[NKS];
   {
     const __bf16* Qr = Q + ((long)b * S + qrow) * ldq + hq * D + 8 * h2;
@@ -458,10 +528,10 @@ __global__ __launch_bounds__(256, 1) void bwd_dq_kernel(
       }
     }
   }
-  float lse_c = 0.f, dl = 0.f;
+  float lse2 = 0.f, dl = 0.f;
   if (qrow < S) {
-    lse_c = -LSE[((long)b * Hq + hq) * S + qrow] * 1.4426950408889634f / scale_log2;
-    dl = -Delta[((long)b * Hq + hq) * S + qrow];
+    lse2 = LSE[((long)b * Hq + hq) * S + qrow] * 1.4426950408889634f;
+    dl = Delta[((long)b * Hq + hq) * S + qrow];
   }
 
   f32x16 dqt[NDB];
@@ -471,60 +541,62 @@ __global__ __launch_bounds__(256, 1) void bwd_dq_kernel(
   const int kend = CAUSAL ? min(S, q0 + QT) : S;
   const int nkt = (kend + KT - 1) / KT;
 
-  Stage<D, KT> sk, sv;
-  sk.load(Kb, ldk, 0, S);
-  sv.load(Vb, ldv, 0, S);
-  sk.store(smem[0][0]);
-  sv.store(smem[0][1]);
+  GStage<D, KT> gk, gv;
+  gk.init(ldk);
+  gv.init(ldv);
+  gk.issue(Kb, smem);
+  gv.issue(Vb, smem + TILE);
   __syncthreads();
 
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int cur = kt & 1;
+  auto body = [&](auto cc, int kt) {
+    constexpr int CUR = decltype(cc)::value;
+    const __bf16* Kt = smem + 2 * CUR * TILE;
+    const __bf16* Vt = Kt + TILE;
     const int k0 = kt * KT;
-    if (kt + 1 < nkt) {
-      sk.load(Kb, ldk, k0 + KT, S);
-      sv.load(Vb, ldv, k0 + KT, S);
+    if (kt + 1 < nkt) {  // LDS-DMA of the next tile runs under this tile's MFMAs
+      gk.issue(Kb + (long)(k0 + KT) * ldk, smem + 2 * (1 - CUR) * TILE);
+      gv.issue(Vb + (long)(k0 + KT) * ldv, smem + 2 * (1 - CUR) * TILE + TILE);
     }
-    if (!(CAUSAL && k0 > qw + 31)) {
-      const __bf16* kt_lds = smem[cur][0];
-      const __bf16* vt_lds = smem[cur][1];
-      // one 32-key half at a time keeps the live accumulator set at 2 x 16 registers
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-        f32x16 s, dp;
+    for (int kb = 0; kb < 2; ++kb) {
+      const int kh = k0 + 32 * kb;
+      if (CAUSAL && kh > qw + 31) continue;  // wave-uniform: this key half is fully masked
+      f32x16 s = f32x16{}, dp = f32x16{};
+      bf16x8 ka = lo.rowk(Kt, 32 * kb, 0), va = lo.rowk(Vt, 32 * kb, 0);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) { s[r] = lse_c; dp[r] = dl; }
-#pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-          const bf16x8 ka = lds_row8(kt_lds, lds_off<D>(kb * 32 + l32, 2 * ks + h2));
-          s = mfma(ka, qf[ks], s);
-          const bf16x8 va = lds_row8(vt_lds, lds_off<D>(kb * 32 + l32, 2 * ks + h2));
-          dp = mfma(va, df[ks], dp);
+      for (int ks = 0; ks < NKS; ++ks) {
+        bf16x8 nk = ka, nv = va;
+        if (ks + 1 < NKS) {
+          nk = lo.rowk(Kt, 32 * kb, ks + 1);
+          nv = lo.rowk(Vt, 32 * kb, ks + 1);
         }
+        s = mfma(ka, qf[ks], s);
+        dp = mfma(va, df[ks], dp);
+        ka = nk; va = nv;
+      }
+      const bool diag = CAUSAL && kh + 31 > qw;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float p = fexp2(s[r] * scale_log2);
-          if constexpr (CAUSAL) {
-            if (k0 + kb * 32 + crow(r, h2) > qrow) p = 0.f;
-          }
-          dp[r] = p * dp[r];
-        }
+      for (int r = 0; r < 16; ++r) {
+        float p = fexp2(fmaf(s[r], scale_log2, -lse2));
+        if (diag && kh + crow(r, h2) > qrow) p = 0.f;
+        dp[r] = p * (dp[r] - dl);
+      }
+      const bf16x8 d0 = pack8(dp, 0), d1 = pack8(dp, 1);
+      bf16x8 kc = lo.tr(Kt, 32 * kb, 0);
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const bf16x8 dsf = pack8(dp, s2);
-#pragma unroll
-          for (int db = 0; db < NDB; ++db) {
-            const bf16x8 kT = tr_frag<D>(kt_lds, kb * 32 + 16 * s2, db * 32, lane);
-            dqt[db] = mfma(kT, dsf, dqt[db]);
-          }
-        }
+      for (int st = 0; st < 2 * NDB; ++st) {
+        const int s2 = st / NDB, db = st % NDB;
+        bf16x8 kn = kc;
+        if (st + 1 < 2 * NDB) kn = lo.tr(Kt, 32 * kb + 16 * ((st + 1) / NDB), (st + 1) % NDB);
+        dqt[db] = mfma(kc, s2 ? d1 : d0, dqt[db]);
+        kc = kn;
       }
     }
-    if (kt + 1 < nkt) {
-      sk.store(smem[cur ^ 1][0]);
-      sv.store(smem[cur ^ 1][1]);
-    }
-    __syncthreads();
+    __syncthreads();  // the DMA'd tile has landed (vmcnt(0)) and this tile is free
+  };
+  for (int kt = 0; kt < nkt; kt += 2) {
+    body(IC<0>{}, kt);
+    if (kt + 1 < nkt) body(IC<1>{}, kt + 1);
   }
 
   if (qrow < S) {
