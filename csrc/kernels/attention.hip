@@ -11,8 +11,8 @@
 //    S^T = K Q^T puts one query per lane, so softmax row statistics are lane-local (plus one
 //    xor-32 exchange), and O^T = V^T P^T reuses the S^T accumulator registers directly as the
 //    B operand (bf16-packed). V^T fragments come from ds_read_b64_tr_b16 (hardware transpose).
-//  * every LDS tile uses one XOR-swizzled image that is conflict-free for both ds_read_b128
-//    row reads and ds_read_b64_tr_b16 transposed reads (row r, 16-B chunk c -> c ^ x(r)).
+//  * every LDS tile uses one sub-tiled, XOR-swizzled image that is conflict-free for both
+//    ds_read_b128 row reads and ds_read_b64_tr_b16 transposed reads (lay_byte below).
 //  * backward is split into two deterministic kernels (no float atomics, so a resumed run is
 //    bit-identical to an uninterrupted one): dK/dV (keys resident per wave, loop over query
 //    tiles and over the Hq/Hkv query heads of the kv head) and dQ (queries resident, loop
@@ -26,40 +26,30 @@ namespace attn {
 
 typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
 
-// XOR swizzle of 16-B chunk c in row r (see header). D=128: 16 chunks/256-B rows;
-// D=64: 8 chunks/128-B rows.
+// LDS image of a [rows][D] bf16 tile: 8-row x 32-column sub-tiles of 512 B, the four 16-B
+// chunks of each 64-B sub-tile row XOR-swizzled by (row >> 2) & 3 (cdna guide T10, image (a)).
+// Conflict-free for ds_read_b128 row reads and ds_read_b64_tr_b16 transposed reads of the
+// 32x32x16 operands, and -- unlike a whole-row XOR -- every k-step / column block / row block
+// (row base a multiple of 16) is a compile-time byte offset from one of two lane-constant bases,
+// so fragment reads need 4 address registers instead of one per k-step.
 template <int D>
-__device__ __forceinline__ int swz(int r, int c) {
-  if constexpr (D == 128) return c ^ (((r & 3) << 2) | ((r >> 2) & 3));
-  else return c ^ ((((r >> 1) & 1) << 2) | ((r >> 2) & 3));
+__device__ __forceinline__ int lay_byte(int r, int ch) {  // byte offset of 16-B chunk ch of row r
+  return (D * 16) * (r >> 3) + 512 * (ch >> 2) + 64 * (r & 7) + 16 * ((ch & 3) ^ ((r >> 2) & 3));
 }
 template <int D>
-__device__ __forceinline__ int lds_off(int r, int c) {  // element offset of chunk c of row r
-  return r * D + swz<D>(r, c) * 8;
+__device__ __forceinline__ void lay_inverse(int o, int& r, int& ch) {  // byte offset -> (row, chunk)
+  const int rg = o / (D * 16), rem = o % (D * 16);
+  const int sub = rem / 512, r7 = (rem % 512) / 64, slot = (rem % 64) / 16;
+  r = 8 * rg + r7;
+  ch = 4 * sub + (slot ^ ((r >> 2) & 3));
 }
 
-__device__ __forceinline__ bf16x8 lds_row8(const __bf16* base, int off) {
-  return *reinterpret_cast<const bf16x8*>(base + off);
+__device__ __forceinline__ bf16x8 lds_read16(const __bf16* tile, int byte_off) {
+  return *reinterpret_cast<const bf16x8*>(reinterpret_cast<const char*>(tile) + byte_off);
 }
-__device__ __forceinline__ i16x4 tr4(const __bf16* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(p));
-}
-
-// Transposed operand fragment for the "accumulator as next operand" pattern: for a tile
-// stored [rows=k][cols=n] in LDS, lane l receives column n = c0 + (l&31) and the 8 rows
-// k = r0 + 8*(j>>2) + 4*(l>>5) + (j&3), j=0..7 (matching the permuted k order of a 32x32
-// accumulator reused as an operand, cdna guide §3).
-template <int D>
-__device__ __forceinline__ bf16x8 tr_frag(const __bf16* tile, int r0, int c0, int lane) {
-  const int g = lane >> 4, i = lane & 15;
-  const int q = i >> 2, p = i & 3;
-  const int row = r0 + 4 * (g >> 1) + q;
-  const int col = c0 + 16 * (g & 1) + 4 * p;
-  const int c = col >> 3, w = col & 7;
-  i16x4 lo = tr4(tile + lds_off<D>(row, c) + w);
-  i16x4 hi = tr4(tile + lds_off<D>(row + 8, c) + w);
-  i16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-  return __builtin_bit_cast(bf16x8, v);
+__device__ __forceinline__ i16x4 tr4(const __bf16* tile, int byte_off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_i16x4*)(reinterpret_cast<const char*>(tile) + byte_off));
 }
 
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
@@ -75,16 +65,27 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& x, int s) {
 
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// lanes i and i^32 exchange through v_permlane32_swap (no LDS round trip)
+__device__ __forceinline__ float half_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float half_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // Stage ROWS x D rows of a [.., ld]-strided bf16 tensor into registers (global loads only).
-template <int D, int ROWS>
+template <int D, int ROWS, int NT = 256>
 struct Stage {
   static constexpr int CH = D / 8;
-  static constexpr int CPT = ROWS * CH / 256;
+  static constexpr int CPT = ROWS * CH / NT;
+  static_assert(CPT * NT == ROWS * CH, "tile must split evenly over the block");
   uint4 r[CPT];
   __device__ __forceinline__ void load(const __bf16* g, long ld, int row0, int nrows_valid) {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const int idx = i * 256 + threadIdx.x;
+      const int idx = i * NT + threadIdx.x;
       const int row = idx / CH, c = idx % CH;
       if (row0 + row < nrows_valid)
         r[i] = *reinterpret_cast<const uint4*>(g + (long)(row0 + row) * ld + c * 8);
@@ -95,16 +96,16 @@ struct Stage {
   __device__ __forceinline__ void store(__bf16* tile) const {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const int idx = i * 256 + threadIdx.x;
+      const int idx = i * NT + threadIdx.x;
       const int row = idx / CH, c = idx % CH;
-      *reinterpret_cast<uint4*>(tile + lds_off<D>(row, c)) = r[i];
+      *reinterpret_cast<uint4*>(reinterpret_cast<char*>(tile) + lay_byte<D>(row, c)) = r[i];
     }
   }
 };
 
-// LDS-DMA staging (global_load_lds_dwordx4) of a ROWS x D tile into the swizzled image. The DMA
+// LDS-DMA staging (global_load_lds_dwordx4) of a ROWS x D tile into the LDS image. The DMA
 // writes 1 KiB per wave-instruction linearly (base + 16 B * lane), so each lane fetches the
-// logical chunk that the swizzle places at its linear position (the XOR swizzle is an involution).
+// (row, chunk) that the image places at its linear position.
 // No VGPR staging; rows must be in bounds (callers guarantee S % tile == 0).
 template <int D, int ROWS>
 struct GStage {
@@ -115,9 +116,9 @@ struct GStage {
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int idx = (i * 4 + wid) * 64 + lane;
-      const int row = idx / CH, pc = idx % CH;
-      off[i] = row * (int)ld + swz<D>(row, pc) * 8;
+      int row, ch;
+      lay_inverse<D>(((i * 4 + wid) * 64 + lane) * 16, row, ch);
+      off[i] = row * (int)ld + ch * 8;
     }
   }
   __device__ __forceinline__ void issue(const __bf16* g, __bf16* tile) const {
@@ -133,36 +134,31 @@ struct GStage {
 // C-layout row of register r for lane half h (32x32 accumulator)
 __device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
-// Lane-invariant LDS offsets (in elements) for the fragment reads of a swizzled [rows][D] tile.
-// Valid for any row base that is a multiple of 16 (the swizzle only depends on row & 15), so the
-// per-tile part of every address is a compile-time constant folded into the ds_read immediate.
+// Lane-constant LDS byte offsets of the MFMA operand reads (image above). For a row base r0 that
+// is a multiple of 16, everything else is a compile-time immediate on the ds_read.
 template <int D>
 struct LaneOff {
-  static constexpr int NKS = D / 16, NDB = D / 32;
-  int row[NKS];            // ds_read_b128 of row (base + l32), chunk 2*ks + h2
-  int trl[NDB], trh[NDB];  // ds_read_b64_tr_b16 blocks of tr_frag(r0 = base, c0 = db*32)
+  int re, ro;  // ds_read_b128 of row l32, chunk 2*ks + h2: even / odd ks
+  int tl, th;  // ds_read_b64_tr_b16 blocks (rows +0..7 / +8..15) of the transposed 32x16 operand
   __device__ __forceinline__ void init(int lane) {
     const int l32 = lane & 31, h2 = lane >> 5;
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) row[ks] = lds_off<D>(l32, 2 * ks + h2);
+    re = lay_byte<D>(l32, h2);
+    ro = lay_byte<D>(l32, 2 + h2);
+    // group g = lane/16, lane 4q+p of the group supplies row 4(g>>1)+q, columns 16(g&1)+4p..+3
     const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-    const int r = 4 * (g >> 1) + q;
-#pragma unroll
-    for (int db = 0; db < NDB; ++db) {
-      const int col = db * 32 + 16 * (g & 1) + 4 * p;
-      trl[db] = lds_off<D>(r, col >> 3) + (col & 7);
-      trh[db] = lds_off<D>(r + 8, col >> 3) + (col & 7);
-    }
+    const int r = 4 * (g >> 1) + q, ch = 2 * (g & 1) + (p >> 1);
+    tl = lay_byte<D>(r, ch) + 8 * (p & 1);
+    th = lay_byte<D>(r + 8, ch) + 8 * (p & 1);
   }
-  // transposed 32x16 operand block of rows [r0, r0+16) (r0 % 16 == 0), cols [db*32, db*32+32)
+  // transposed operand: rows [r0, r0+16) (r0 % 16 == 0), columns [32 db, 32 db + 32)
   __device__ __forceinline__ bf16x8 tr(const __bf16* tile, int r0, int db) const {
-    const i16x4 lo = tr4(tile + r0 * D + trl[db]);
-    const i16x4 hi = tr4(tile + r0 * D + trh[db]);
+    const i16x4 lo = tr4(tile, r0 * 2 * D + 512 * db + tl);
+    const i16x4 hi = tr4(tile, r0 * 2 * D + 512 * db + th);
     return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
   }
-  // row operand: rows [r0, r0+32) (r0 % 16 == 0), k-step ks
+  // row operand: rows [r0, r0+32) (r0 % 16 == 0), k-step ks (columns 16 ks .. 16 ks + 15)
   __device__ __forceinline__ bf16x8 rowk(const __bf16* tile, int r0, int ks) const {
-    return lds_row8(tile, r0 * D + row[ks]);
+    return lds_read16(tile, r0 * 2 * D + 512 * (ks >> 1) + ((ks & 1) ? ro : re));
   }
 };
 
@@ -172,12 +168,14 @@ using IC = std::integral_constant<int, N>;
 // ======================================================================================
 // Forward
 // ======================================================================================
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void fwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K,
-                                                     const __bf16* __restrict__ V, __bf16* __restrict__ O,
-                                                     float* __restrict__ LSE, int S, int Hq, int Hkv, long ldq,
-                                                     long ldk, long ldv, long ldo, float scale_log2) {
-  constexpr int KT = 64, QT = 128;
+// Block = NW waves x 32 query rows (NW = 8: one 512-thread block per CU, 2 waves per SIMD), so
+// each staged K/V tile feeds 8 waves' MFMAs.
+template <int D, bool CAUSAL, int NW>
+__global__ __launch_bounds__(NW * 64, 2) void fwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K,
+                                                         const __bf16* __restrict__ V, __bf16* __restrict__ O,
+                                                         float* __restrict__ LSE, int S, int Hq, int Hkv, long ldq,
+                                                         long ldk, long ldv, long ldo, float scale_log2) {
+  constexpr int KT = 64, QT = 32 * NW;
   constexpr int NKS = D / 16, NDB = D / 32, TILE = KT * D;
   __shared__ __attribute__((aligned(16))) __bf16 smem[4 * TILE];  // K0 V0 K1 V1
 
@@ -210,12 +208,14 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const __bf16* __restrict__ 
   const int kend = CAUSAL ? min(S, q0 + QT) : S;
   const int nkt = (kend + KT - 1) / KT;
 
-  Stage<D, KT> sk, sv;
+  Stage<D, KT, NW * 64> sk, sv;
   sk.load(Kb, ldk, 0, S);
   sv.load(Vb, ldv, 0, S);
   sk.store(smem);
   sv.store(smem + TILE);
   __syncthreads();
+  // the younger half of an 8-wave block loses VALU arbitration; one static priority bump evens it
+  if (NW == 8 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
 
   auto body = [&](auto cc, int kt) {
     constexpr int CUR = decltype(cc)::value;
@@ -253,7 +253,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const __bf16* __restrict__ 
       float mx = -INFINITY;
 #pragma unroll
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, fmaxf(s0[r], s1[r]));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * scale_log2;
+      mx = half_max(mx) * scale_log2;
       // exact deferred rescale: only when some row's running max grows in this wave
       if (!__all(mx <= m_i)) {
         const float m_new = fmaxf(m_i, mx);
@@ -270,7 +270,7 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(const __bf16* __restrict__ 
         s1[r] = fexp2(fmaf(s1[r], scale_log2, -m_i));
         rs += s0[r] + s1[r];
       }
-      l_i += rs + __shfl_xor(rs, 32, 64);
+      l_i += half_sum(rs);
       const bf16x8 p00 = pack8(s0, 0), p01 = pack8(s0, 1), p10 = pack8(s1, 0), p11 = pack8(s1, 1);
       // O^T[d][q] += V^T[d][key] P^T[key][q]; V^T fragments prefetched one MFMA ahead
       bf16x8 vc = lo.tr(Vt, 0, 0);
@@ -362,11 +362,12 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(
   constexpr int KB = 128, QT = 32;
   constexpr int NKS = D / 16, NDB = D / 32;
   constexpr int KVT = KB * D, QDT = QT * D;
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * KVT + 2 * QDT];  // K V Q dO
-  __bf16* const Ks = smem;
-  __bf16* const Vs = smem + KVT;
-  __bf16* const Qs = smem + 2 * KVT;
-  __bf16* const Ds = smem + 2 * KVT + QDT;
+  // Q and dO first: their (transposed) reads then use 16-bit immediate offsets off one base
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * KVT + 2 * QDT];  // Q dO K V
+  __bf16* const Qs = smem;
+  __bf16* const Ds = smem + QDT;
+  __bf16* const Ks = smem + 2 * QDT;
+  __bf16* const Vs = smem + 2 * QDT + KVT;
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h2 = lane >> 5, l32 = lane & 31;
   const int nkb = S / KB;
@@ -400,7 +401,8 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(
   // lane reads the row constant of query row l32 of the tile: lse*log2e (h2 = 0) or delta (h2 = 1)
   const float rc_mul = h2 ? 1.f : 1.4426950408889634f;
   const float* rc_base = (h2 ? Delta : LSE) + (long)b * Hq * S + l32;
-  const int bp_base = 4 * (4 * h2);  // ds_bpermute byte address of lane crow(0, h2)
+  int bp_base = 4 * (4 * h2);  // ds_bpermute byte address of lane crow(0, h2)
+  asm volatile("" : "+v"(bp_base));  // opaque: per-row offsets then fold into the ds offset field
 
   Stage<D, QT> sq, sd;
   auto stage_load = [&](int it) {
@@ -626,11 +628,12 @@ hipError_t pra_attn_fwd(const void* q, const void* k, const void* v, void* o, fl
                         hipStream_t st) {
   if (S % 64 || (D != 64 && D != 128) || Hq % Hkv) return hipErrorInvalidValue;
   if (ldq % 8 || ldk % 8 || ldv % 8 || ldo % 4) return hipErrorInvalidValue;
-  const int nqt = (S + 127) / 128;
-  dim3 grid(nqt * Hq * B), block(256);
+  constexpr int NW = 8;
+  const int nqt = (S + 32 * NW - 1) / (32 * NW);
+  dim3 grid(nqt * Hq * B), block(NW * 64);
   const float sl2 = scale * 1.4426950408889634f;
 #define LAUNCH(DD, CC)                                                                                        \
-  hipLaunchKernelGGL((fwd_kernel<DD, CC>), grid, block, 0, st, (const __bf16*)q, (const __bf16*)k,             \
+  hipLaunchKernelGGL((fwd_kernel<DD, CC, NW>), grid, block, 0, st, (const __bf16*)q, (const __bf16*)k,             \
                      (const __bf16*)v, (__bf16*)o, lse, S, Hq, Hkv, ldq, ldk, ldv, ldo, sl2)
   if (D == 128) { if (causal) LAUNCH(128, true); else LAUNCH(128, false); }
   else { if (causal) LAUNCH(64, true); else LAUNCH(64, false); }

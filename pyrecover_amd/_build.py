@@ -53,6 +53,12 @@ def _run(cmd):
     return r
 
 
+# Per-file code-generation flags. attention.hip: no NaN semantics for fmaxf (drops the canonicalising
+# v_max before every max on MFMA results) and no SLP packing of f32 adds (packed f32 VALU beside
+# MFMAs costs more issue cycles than the scalar form).
+EXTRA_FLAGS = {"attention.hip": ["-fno-honor-nans", "-fno-slp-vectorize"]}
+
+
 def build(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:
     os.makedirs(BUILD, exist_ok=True)
     inc, libdir, abi = _torch_paths()
@@ -74,7 +80,7 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:
         if not stale:
             continue
         if src.endswith(".hip"):
-            cmd = [HIPCC] + common + ["-c", src, "-o", obj]
+            cmd = [HIPCC] + common + EXTRA_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj]
         else:  # host translation units (torch + pybind headers); compiled as HIP host code
             cmd = [HIPCC] + common + torch_flags + ["-x", "hip", "-c", src, "-o", obj]
         tasks.append(cmd)
