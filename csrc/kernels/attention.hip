@@ -6,17 +6,23 @@
 // [B, S, H, D] views with an arbitrary token stride, so no transpose/contiguous copies.
 //
 // Design (all MFMA work on v_mfma_f32_32x32x16_bf16, wave64):
-//  * forward: 256-thread block = 4 waves = 128 query rows (32 per wave); K/V tiles of 64 keys
-//    staged global->regs->LDS, double-buffered, one barrier per tile. "Swapped" products:
+//  * forward: 512-thread block = 8 waves = 256 query rows (32 per wave, 2 waves per SIMD); K/V
+//    tiles of 64 keys staged global->regs->LDS (issue-early / write-late), double-buffered, one
+//    barrier per tile; online softmax with an exact deferred rescale (skipped when no row max
+//    grows). "Swapped" products:
 //    S^T = K Q^T puts one query per lane, so softmax row statistics are lane-local (plus one
 //    xor-32 exchange), and O^T = V^T P^T reuses the S^T accumulator registers directly as the
 //    B operand (bf16-packed). V^T fragments come from ds_read_b64_tr_b16 (hardware transpose).
 //  * every LDS tile uses one sub-tiled, XOR-swizzled image that is conflict-free for both
 //    ds_read_b128 row reads and ds_read_b64_tr_b16 transposed reads (lay_byte below).
 //  * backward is split into two deterministic kernels (no float atomics, so a resumed run is
-//    bit-identical to an uninterrupted one): dK/dV (keys resident per wave, loop over query
-//    tiles and over the Hq/Hkv query heads of the kv head) and dQ (queries resident, loop
-//    over key tiles). P is recomputed from the saved log-sum-exp.
+//    bit-identical to an uninterrupted one): dK/dV (K/V of 128 keys resident in LDS, dK/dV
+//    accumulators in registers, loop over query tiles and over the Hq/Hkv query heads of the kv
+//    head) and dQ (queries resident, K/V tiles by LDS-DMA, loop over key tiles). P is
+//    recomputed from the saved log-sum-exp. Both run at 2 waves per SIMD with no spills.
+//
+// Measured on MI355X (tools/attn_bench.py, B4 S2048 H32 D128 causal): fwd 0.214 ms (640 TF),
+// bwd 0.645 ms (530 TF at the 2.5x-forward convention); B16 H64/8 non-causal fwd 835 TF.
 #include "common.h"
 
 #include <type_traits>
