@@ -36,6 +36,8 @@ def parse():
     ap.add_argument("--profile-steps", type=int, default=0, help="emit roctx ranges for this many steps")
     ap.add_argument("--no-overlap-optimizer", action="store_true",
                     help="AdamW after backward instead of per bucket during backward")
+    ap.add_argument("--phase-timing", action="store_true",
+                    help="record device events around forward / backward / optimizer of each timed step")
     ap.add_argument("--gemm-tuning", choices=["auto", "off", "tune"], default="auto",
                     help="hipBLASLt solution table (tuning/): auto = use the committed table if present")
     return ap.parse_args()
@@ -91,14 +93,26 @@ def main():
         t = torch.randint(0, cfg.vocab_size, (B, S + 1), device=dev, generator=gen)
         return t[:, :-1], t[:, 1:]
 
-    def step():
+    phases = []
+
+    def step(timed=False):
         x, y = batch()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if timed else None
         opt.zero_grad()
+        if ev:
+            ev[0].record()
         loss = model(x, labels=y)
+        if ev:
+            ev[1].record()
         loss.backward()
         reducer.finish()
+        if ev:
+            ev[2].record()
         opt.step()
         sched.step()
+        if ev:
+            ev[3].record()
+            phases.append(ev)
         return loss
 
     for _ in range(args.warmup):
@@ -111,7 +125,7 @@ def main():
     for i in range(args.steps):
         if args.profile_steps and i < args.profile_steps:
             torch.cuda.nvtx.range_push(f"step{i}")
-        loss = step()
+        loss = step(timed=args.phase_timing)
         if args.profile_steps and i < args.profile_steps:
             torch.cuda.nvtx.range_pop()
     torch.cuda.synchronize()
@@ -152,6 +166,10 @@ def main():
             "peak_mem_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1),
             "gemm_table": bool(torch.cuda.tunable.is_enabled()),
         }
+        if phases:
+            n = len(phases)
+            out["phase_ms"] = {k: round(sum(e[i].elapsed_time(e[i + 1]) for e in phases) / n, 2)
+                               for i, k in enumerate(("forward", "backward+reduce", "optimizer"))}
         print(json.dumps(out), flush=True)
     from pyrecover_amd.utils.gemm_tuning import flush_tuning
 

@@ -1,0 +1,59 @@
+#!/usr/bin/env python
+"""Standalone throughput of the bench's library GEMMs (hipBLASLt via torch.mm) on random bf16
+operands, each shape timed back to back (--iters) after warmup, with the committed TunableOp
+table (default) or the library heuristic (--no-table). Compares isolated GEMM speed with what the
+same shapes reach inside a training step (rocprofv3 kernel stats)."""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tokens", type=int, default=16384)
+    ap.add_argument("--dim", type=int, default=4096)
+    ap.add_argument("--ffn", type=int, default=11008)
+    ap.add_argument("--vocab", type=int, default=32000)
+    ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--no-table", action="store_true")
+    a = ap.parse_args()
+    from pyrecover_amd.utils.gemm_tuning import configure_gemm_tuning
+
+    configure_gemm_tuning("off" if a.no_table else "auto")
+    dev = torch.device("cuda", 0)
+    T, Dm, F, V = a.tokens, a.dim, a.ffn, a.vocab
+    outs = {"qkv": 3 * Dm, "wo": Dm, "w13": 2 * F, "w2": Dm, "head": V}
+    ins = {"qkv": Dm, "wo": Dm, "w13": Dm, "w2": F, "head": Dm}
+    res = {}
+    for name in outs:
+        n_out, n_in = outs[name], ins[name]
+        x = torch.randn(T, n_in, device=dev).bfloat16()
+        w = torch.randn(n_out, n_in, device=dev).bfloat16()
+        dy = torch.randn(T, n_out, device=dev).bfloat16()
+        cases = {"fwd": lambda: torch.mm(x, w.t()), "dgrad": lambda: torch.mm(dy, w),
+                 "wgrad": lambda: torch.mm(dy.t(), x)}
+        for cname, fn in cases.items():
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / a.iters
+            res[f"{name}_{cname}"] = {"ms": round(ms, 4), "tflops": round(2 * T * n_in * n_out / ms / 1e9, 1)}
+        del x, w, dy
+    tot_ms = sum(v["ms"] for k, v in res.items() if not k.startswith("head")) * 32 + sum(
+        v["ms"] for k, v in res.items() if k.startswith("head"))
+    print(json.dumps({"table": not a.no_table, "gemm_ms_per_step": round(tot_ms, 1), "shapes": res}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
