@@ -7,9 +7,31 @@
 #include <c10/hip/HIPStream.h>
 #include <c10/core/DeviceGuard.h>
 
+#include <roctracer/roctx.h>
+
+#include <atomic>
+#include <cstdlib>
+
 #include "kernels/launchers.h"
 
 namespace {
+
+// roctx range per op ("pyrecover::attn_fwd", ...) so rocprofv3 --marker-trace / --selected-regions
+// timelines show which framework op launched each kernel. Off by default (one branch per op);
+// enabled by set_roctx(True) (train.py --profile) or PYRECOVER_ROCTX=1.
+std::atomic<bool> g_roctx{[] {
+  const char* e = std::getenv("PYRECOVER_ROCTX");
+  return e != nullptr && e[0] == '1';
+}()};
+struct Range {
+  bool on;
+  explicit Range(const char* name) : on(g_roctx.load(std::memory_order_relaxed)) {
+    if (on) roctxRangePushA(name);
+  }
+  ~Range() {
+    if (on) roctxRangePop();
+  }
+};
 
 int dt(const at::Tensor& t) {
   switch (t.scalar_type()) {
@@ -47,6 +69,7 @@ void check_row_major(const at::Tensor& t, const char* name) {
 // ---------------------------------------------------------------------------------------
 std::vector<at::Tensor> rmsnorm_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& delta, const at::Tensor& w,
                                     double eps) {
+  const Range range_("pyrecover::rmsnorm_fwd");
   check_dev(x, "x");
   TORCH_CHECK(x.is_contiguous() && w.is_contiguous(), "rmsnorm_fwd: x and w must be contiguous");
   const int64_t D = x.size(-1);
@@ -74,6 +97,7 @@ std::vector<at::Tensor> rmsnorm_fwd(const at::Tensor& x, const c10::optional<at:
 
 at::Tensor rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at::Tensor& w, const at::Tensor& rstd,
                        const c10::optional<at::Tensor>& dres, at::Tensor dw, bool accumulate) {
+  const Range range_("pyrecover::rmsnorm_bwd");
   check_dev(dy, "dy");
   TORCH_CHECK(dy.is_contiguous() && h.is_contiguous() && dy.sizes() == h.sizes(), "rmsnorm_bwd: dy/h mismatch");
   const int64_t D = h.size(-1);
@@ -106,6 +130,7 @@ at::Tensor rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at::Tens
 // LayerNorm: returns (h, y, mean, rstd)
 std::vector<at::Tensor> layernorm_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& delta, const at::Tensor& w,
                                       const at::Tensor& b, double eps) {
+  const Range range_("pyrecover::layernorm_fwd");
   check_dev(x, "x");
   TORCH_CHECK(x.is_contiguous() && w.is_contiguous() && b.is_contiguous(), "layernorm_fwd: contiguous");
   const int64_t D = x.size(-1);
@@ -135,6 +160,7 @@ std::vector<at::Tensor> layernorm_fwd(const at::Tensor& x, const c10::optional<a
 // dwb: 2*D contiguous output [dw | db]
 at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at::Tensor& w, const at::Tensor& mean,
                          const at::Tensor& rstd, const c10::optional<at::Tensor>& dres, at::Tensor dwb, bool accumulate) {
+  const Range range_("pyrecover::layernorm_bwd");
   check_dev(dy, "dy");
   TORCH_CHECK(dy.is_contiguous() && h.is_contiguous() && dy.sizes() == h.sizes(), "layernorm_bwd: dy/h mismatch");
   const int64_t D = h.size(-1);
@@ -163,6 +189,7 @@ at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at::Te
 // In-place RoPE on the first `ncols` columns of each row of a 2-D [tokens, ld] buffer.
 void rope_(at::Tensor x2d, int64_t ncols, const at::Tensor& tab, int64_t head_dim, int64_t seq_len,
            int64_t pos_offset, bool inverse) {
+  const Range range_("pyrecover::rope");
   check_dev(x2d, "x");
   check_row_major(x2d, "rope x");
   TORCH_CHECK(tab.scalar_type() == at::kFloat && tab.is_contiguous(), "rope: table must be contiguous fp32");
@@ -178,6 +205,7 @@ void rope_(at::Tensor x2d, int64_t ncols, const at::Tensor& tab, int64_t head_di
 
 // gu: [T, 2F] (gate | up) -> y [T, F]
 at::Tensor swiglu_fwd(const at::Tensor& gu) {
+  const Range range_("pyrecover::swiglu_fwd");
   check_dev(gu, "gu");
   check_row_major(gu, "gu");
   TORCH_CHECK(gu.size(1) % 16 == 0, "swiglu: 2F must be a multiple of 16");
@@ -193,6 +221,7 @@ at::Tensor swiglu_fwd(const at::Tensor& gu) {
 
 // dgu may alias gu (in-place backward).
 at::Tensor swiglu_bwd(const at::Tensor& dy, const at::Tensor& gu, c10::optional<at::Tensor> out) {
+  const Range range_("pyrecover::swiglu_bwd");
   check_dev(gu, "gu");
   check_row_major(gu, "gu");
   check_row_major(dy, "dy");
@@ -213,6 +242,7 @@ at::Tensor swiglu_bwd(const at::Tensor& dy, const at::Tensor& gu, c10::optional<
 }
 
 at::Tensor embedding_fwd(const at::Tensor& ids, const at::Tensor& W) {
+  const Range range_("pyrecover::embedding_fwd");
   check_dev(W, "W");
   TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous() && ids.device() == W.device(),
               "embedding: ids must be contiguous int64 on the weight's device");
@@ -229,6 +259,7 @@ at::Tensor embedding_fwd(const at::Tensor& ids, const at::Tensor& W) {
 
 // Deterministic dense embedding gradient into dW (overwrites unless accumulate).
 void embedding_bwd(const at::Tensor& ids, const at::Tensor& dout, at::Tensor dW, bool accumulate) {
+  const Range range_("pyrecover::embedding_bwd");
   check_dev(dW, "dW");
   TORCH_CHECK(dW.is_contiguous() && dout.is_contiguous() && dout.size(-1) == dW.size(1), "embedding_bwd: shapes");
   TORCH_CHECK(dout.numel() / dW.size(1) == ids.numel(), "embedding_bwd: ids/dout mismatch");
@@ -248,6 +279,7 @@ void embedding_bwd(const at::Tensor& ids, const at::Tensor& dout, at::Tensor dW,
 
 // logits [T, V] (row stride ld), labels [T] -> (lse [T], loss_row [T], stats [2] = {mean loss, n_valid})
 std::vector<at::Tensor> xent_fwd(const at::Tensor& logits, const at::Tensor& labels, int64_t ignore_index) {
+  const Range range_("pyrecover::xent_fwd");
   check_dev(logits, "logits");
   check_row_major(logits, "logits");
   TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_contiguous() && labels.numel() == logits.size(0),
@@ -266,6 +298,7 @@ std::vector<at::Tensor> xent_fwd(const at::Tensor& logits, const at::Tensor& lab
 
 void xent_bwd_(at::Tensor logits, const at::Tensor& labels, const at::Tensor& lse, const at::Tensor& stats,
                const at::Tensor& grad_out, int64_t ignore_index) {
+  const Range range_("pyrecover::xent_bwd");
   check_dev(logits, "logits");
   check_row_major(logits, "logits");
   TORCH_CHECK(grad_out.scalar_type() == at::kFloat && grad_out.numel() == 1 && grad_out.is_cuda(),
@@ -288,6 +321,7 @@ void xent_bwd_(at::Tensor logits, const at::Tensor& labels, const at::Tensor& ls
 void adamw_flat_(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, double lr, double b1, double b2,
                  double eps, double wd, double bc1, double bc2_sqrt, double gscale,
                  const c10::optional<at::Tensor>& gscale_dev) {
+  const Range range_("pyrecover::adamw_flat");
   check_dev(p, "p");
   TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous(), "adamw: contiguous");
   TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(), "adamw: sizes");
@@ -310,6 +344,7 @@ void adamw_flat_(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, 
 
 // returns fp32 [2] = {norm, clip_coef}
 at::Tensor grad_norm(const at::Tensor& x, double max_norm, double pre_scale) {
+  const Range range_("pyrecover::grad_norm");
   check_dev(x, "x");
   TORCH_CHECK(x.is_contiguous(), "grad_norm: contiguous");
   const c10::DeviceGuard guard(x.device());
@@ -333,6 +368,7 @@ void check_bshd(const at::Tensor& t, const char* name, int64_t B, int64_t S, int
 
 std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale,
                                  bool causal) {
+  const Range range_("pyrecover::attn_fwd");
   check_dev(q, "q");
   const int64_t B = q.size(0), S = q.size(1), Hq = q.size(2), D = q.size(3), Hkv = k.size(2);
   check_bshd(q, "q", B, S, Hq, D);
@@ -357,6 +393,7 @@ std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const
 void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const at::Tensor& o,
               const at::Tensor& dout, const at::Tensor& lse, at::Tensor dq, at::Tensor dk, at::Tensor dv, double scale,
               bool causal) {
+  const Range range_("pyrecover::attn_bwd");
   check_dev(q, "q");
   const int64_t B = q.size(0), S = q.size(1), Hq = q.size(2), D = q.size(3), Hkv = k.size(2);
   check_bshd(q, "q", B, S, Hq, D);
@@ -386,6 +423,8 @@ void register_ckpt_engine(pybind11::module& m);  // csrc/runtime/ckpt_engine.cpp
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "pyrecover_amd native ops (HIP/gfx950 kernels + checkpoint engine)";
+  m.def("set_roctx", [](bool on) { g_roctx.store(on); });
+  m.def("roctx_enabled", []() { return g_roctx.load(); });
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
   m.def("layernorm_fwd", &layernorm_fwd);

@@ -93,7 +93,7 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:
     if tasks or force or not os.path.exists(out) or any(os.path.getmtime(o) > os.path.getmtime(out) for o in objs):
         link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out + ".tmp"] + objs + [
             f"-L{libdir}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
-            f"-Wl,-rpath,{libdir}", "-lz", "-lcrypto", "-lpthread"]
+            f"-Wl,-rpath,{libdir}", "-lz", "-lcrypto", "-lpthread", f"-L{os.path.join(ROCM, 'lib')}", "-lroctx64"]
         _run(link)
         os.replace(out + ".tmp", out)
     return out

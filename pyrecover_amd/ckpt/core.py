@@ -245,6 +245,21 @@ def wait_all():
 def fence_all():
     for c in Checkpointer._instances.values():
         c.fence()
+    if os.environ.get("PYRECOVER_DEBUG_CKPT") == "1":
+        assert_snapshots_landed()
+
+
+def assert_snapshots_landed():
+    """Debug assertion (PYRECOVER_DEBUG_CKPT=1): block until the compute stream has
+    passed the snapshot fence and check every staged D2H chunk has completed, i.e. the optimizer
+    step that follows cannot mutate parameters that are still being copied out."""
+    import torch
+
+    for c in Checkpointer._instances.values():
+        if c.staged and c.device_index >= 0:
+            torch.cuda.current_stream(c.device_index).synchronize()
+            if not c.engine.staged_complete():
+                raise RuntimeError("pyrecover: optimizer step would overtake an in-flight checkpoint snapshot")
 
 
 # ------------------------------------------------------------------------------------------

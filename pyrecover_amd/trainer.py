@@ -49,14 +49,25 @@ logger = logging.getLogger("pyrecover")
 log_rank0 = D.log_rank0
 
 
+def _set_op_ranges(on: bool):
+    """Per-op roctx ranges inside the HIP extension ("pyrecover::attn_fwd", ...)."""
+    from . import _ext
+
+    if _ext.available():
+        _ext.native().set_roctx(on)
+
+
 def _profiler_start():
+    """Profiler window (reference train.py:237-239): hip profiler start + per-op roctx ranges."""
     try:
         torch.cuda.cudart().cudaProfilerStart()
     except Exception:  # pragma: no cover
         pass
+    _set_op_ranges(True)
 
 
 def _profiler_stop():
+    _set_op_ranges(False)
     try:
         torch.cuda.cudart().cudaProfilerStop()
     except Exception:  # pragma: no cover

@@ -200,3 +200,19 @@ def test_kill_during_save_never_corrupts_latest(tmp_path):
     assert not (tmp_path / "default-exp" / "ckpt_4.pt").exists()
     r = _tiny_run(tmp_path, 4, ["--resume-from-checkpoint", "latest", "--verify-checkpoints"])
     assert r["step"] == 4
+
+
+def test_op_roctx_ranges_toggle():
+    """Per-op roctx ranges are switchable at runtime; the trainer turns them on for
+    the --profile window."""
+    from pyrecover_amd import _ext
+
+    if not _ext.available():
+        pytest.skip("native extension not built")
+    C = _ext.native()
+    was = C.roctx_enabled()
+    C.set_roctx(True)
+    assert C.roctx_enabled()
+    C.set_roctx(False)
+    assert not C.roctx_enabled()
+    C.set_roctx(was)
