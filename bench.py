@@ -36,6 +36,8 @@ def parse():
     ap.add_argument("--profile-steps", type=int, default=0, help="emit roctx ranges for this many steps")
     ap.add_argument("--no-overlap-optimizer", action="store_true",
                     help="AdamW after backward instead of per bucket during backward")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the step into a HIP graph after the warmup steps (train.py --compile)")
     ap.add_argument("--phase-timing", action="store_true",
                     help="record device events around forward / backward / optimizer of each timed step")
     ap.add_argument("--gemm-tuning", choices=["auto", "off", "tune"], default="auto",
@@ -94,9 +96,20 @@ def main():
         return t[:, :-1], t[:, 1:]
 
     phases = []
+    sg = None
+    if args.graph:
+        from pyrecover_amd.graph import StepGraph
+
+        sg = StepGraph(model, opt, reducer)
+    n_eager = [0]
 
     def step(timed=False):
         x, y = batch()
+        if sg is not None and n_eager[0] >= 2:
+            loss = sg.step(x, y)
+            sched.step()
+            return loss
+        n_eager[0] += 1
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if timed else None
         opt.zero_grad()
         if ev:
@@ -165,6 +178,7 @@ def main():
             "final_loss": round(final_loss, 4),
             "peak_mem_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1),
             "gemm_table": bool(torch.cuda.tunable.is_enabled()),
+            "hip_graph": bool(args.graph),
         }
         if phases:
             n = len(phases)

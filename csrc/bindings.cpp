@@ -320,7 +320,7 @@ void xent_bwd_(at::Tensor logits, const at::Tensor& labels, const at::Tensor& ls
 
 void adamw_flat_(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, double lr, double b1, double b2,
                  double eps, double wd, double bc1, double bc2_sqrt, double gscale,
-                 const c10::optional<at::Tensor>& gscale_dev) {
+                 const c10::optional<at::Tensor>& gscale_dev, const c10::optional<at::Tensor>& hyper_dev) {
   const Range range_("pyrecover::adamw_flat");
   check_dev(p, "p");
   TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous(), "adamw: contiguous");
@@ -336,9 +336,15 @@ void adamw_flat_(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, 
     same_dev(p, *gscale_dev, "gscale_dev");
     gsd = gscale_dev->data_ptr<float>();
   }
+  const float* hyd = nullptr;
+  if (hyper_dev.has_value()) {
+    TORCH_CHECK(hyper_dev->scalar_type() == at::kFloat && hyper_dev->numel() >= 3, "adamw: hyper_dev fp32[3]");
+    same_dev(p, *hyper_dev, "hyper_dev");
+    hyd = hyper_dev->data_ptr<float>();
+  }
   check(pra_adamw_flat(dt(p), dt(m), p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), (float)lr,
                        (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1, (float)bc2_sqrt, (float)gscale, gsd,
-                       stream_of(p)),
+                       hyd, stream_of(p)),
         "adamw_flat");
 }
 
@@ -436,7 +442,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("embedding_bwd", &embedding_bwd);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd_", &xent_bwd_);
-  m.def("adamw_flat_", &adamw_flat_);
+  namespace py = pybind11;
+  m.def("adamw_flat_", &adamw_flat_, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("lr"),
+        py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("bc1"), py::arg("bc2_sqrt"),
+        py::arg("gscale"), py::arg("gscale_dev") = py::none(), py::arg("hyper_dev") = py::none());
   m.def("grad_norm", &grad_norm);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);

@@ -11,7 +11,9 @@
 //   p  = p - (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)
 //
 // `gscale` pre-multiplies the gradient (1/world_size after a SUM all-reduce, and/or a
-// clip coefficient read from device memory when `gscale_dev` is non-null).
+// clip coefficient read from device memory when `gscale_dev` is non-null). `hyper_dev`, when
+// non-null, supplies {lr, bc1, bc2_sqrt} from device memory so a captured HIP graph of the
+// training step replays with the current learning rate and bias corrections.
 #include "common.h"
 
 namespace pra {
@@ -20,8 +22,14 @@ template <typename P, typename S>
 __global__ __launch_bounds__(256) void adamw_kernel(P* __restrict__ p, const P* __restrict__ g, S* __restrict__ m,
                                                     S* __restrict__ v, long n, float lr, float b1, float b2,
                                                     float eps, float wd, float bc1, float bc2_sqrt, float gscale,
-                                                    const float* __restrict__ gscale_dev) {
+                                                    const float* __restrict__ gscale_dev,
+                                                    const float* __restrict__ hyper_dev) {
   const float gs = gscale_dev ? gscale * gscale_dev[0] : gscale;
+  if (hyper_dev) {  // step-dependent scalars from device memory (graph-captured step)
+    lr = hyper_dev[0];
+    bc1 = hyper_dev[1];
+    bc2_sqrt = hyper_dev[2];
+  }
   const float decay = 1.f - lr * wd;
   const float step_size = lr / bc1;
   const long n8 = n / 8;
@@ -99,14 +107,15 @@ extern "C" {
 // pdtype: param/grad dtype; sdtype: moment dtype
 hipError_t pra_adamw_flat(int pdtype, int sdtype, void* p, const void* g, void* m, void* v, long n, float lr,
                           float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt, float gscale,
-                          const float* gscale_dev, hipStream_t s) {
+                          const float* gscale_dev, const float* hyper_dev, hipStream_t s) {
   long blocks = (n / 8 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
   if (pdtype != sdtype) return hipErrorInvalidValue;
   PRA_DISPATCH_FLOAT(pdtype, T,
                      hipLaunchKernelGGL((pra::adamw_kernel<T, T>), dim3(blocks), dim3(256), 0, s, (T*)p, (const T*)g,
-                                        (T*)m, (T*)v, n, lr, b1, b2, eps, wd, bc1, bc2_sqrt, gscale, gscale_dev));
+                                        (T*)m, (T*)v, n, lr, b1, b2, eps, wd, bc1, bc2_sqrt, gscale, gscale_dev,
+                                        hyper_dev));
   return hipGetLastError();
 }
 

@@ -59,7 +59,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--grad-max-norm", type=float, default=1, help="used only with --clip-grad (reference: unused)")
     p.add_argument("--model-dtype", type=str, default="bf16", choices=sorted(PRECISION_STR_TO_DTYPE))
     p.add_argument("--compile", action="store_true",
-                   help="accepted for CLI parity; the step is HIP-kernel based (no Triton/Inductor)")
+                   help="capture the whole training step into a HIP graph and replay it (the reference's "
+                        "torch.compile flag; no Triton/Inductor)")
+    p.add_argument("--compile-warmup-steps", type=int, default=2,
+                   help="eager steps before the step graph is captured (--compile)")
     p.add_argument("--distributed", action="store_true")
     p.add_argument("--checkpoint-dir", type=str, default="checkpoints/")
     p.add_argument("--checkpoint-frequency", type=int, default=10)

@@ -43,6 +43,35 @@ class FlatAdamW(torch.optim.AdamW):
         self._in_step = False
         self._done_ranges = []
         self.pre_update_fences = []  # callables run on the update stream before any update
+        # graph mode (train.py --compile): step-dependent scalars come from device memory
+        self.graph_mode = False
+        self.hyper: Optional[torch.Tensor] = None
+        self._hyper_ring = []
+        self._hyper_slot = 0
+
+    # --- captured-step (HIP graph) support ---------------------------------------------------
+    def enable_graph_mode(self):
+        """Kernels read {lr, bc1, bc2_sqrt} from ``self.hyper`` (device fp32[3]) instead of
+        launch arguments, and the host step counter advances in :meth:`begin_graph_step`, so one
+        captured step replays correctly at every later step and learning rate."""
+        if not self.flat.data.is_cuda:
+            raise RuntimeError("graph mode needs the parameters on a GPU")
+        self.graph_mode = True
+        dev = self.flat.data.device
+        self.hyper = torch.zeros(3, dtype=torch.float32, device=dev)
+        # pinned staging ring: a slot is rewritten only after its previous H2D copy completed
+        self._hyper_ring = [(torch.zeros(3, dtype=torch.float32).pin_memory(), torch.cuda.Event()) for _ in range(4)]
+
+    def begin_graph_step(self):
+        """Host side of one replayed step: advance the step count and upload the scalars."""
+        self._step += 1
+        lr, _, _, _, _, bc1, bc2_sqrt = self._coeffs()
+        host, ev = self._hyper_ring[self._hyper_slot]
+        self._hyper_slot = (self._hyper_slot + 1) % len(self._hyper_ring)
+        ev.synchronize()
+        host[0], host[1], host[2] = lr, bc1, bc2_sqrt
+        self.hyper.copy_(host, non_blocking=True)
+        ev.record()
 
     # --- overlapped update (optimizer-in-backward) ----------------------------------------
     def enable_overlap(self, reducer):
@@ -65,7 +94,7 @@ class FlatAdamW(torch.optim.AdamW):
         if f.data.is_cuda:
             _ext.require_for(f.data).adamw_flat_(f.data[lo:hi], f.grad[lo:hi], self.exp_avg[lo:hi],
                                                  self.exp_avg_sq[lo:hi], lr, b1, b2, eps, wd, bc1, bc2_sqrt,
-                                                 self.grad_scale, self.grad_scale_dev)
+                                                 self.grad_scale, self.grad_scale_dev, self.hyper)
         else:
             self._step_reference(lr, b1, b2, eps, wd, bc1, bc2_sqrt, lo, hi)
 
@@ -74,7 +103,8 @@ class FlatAdamW(torch.optim.AdamW):
             return  # clipping needs the global norm first: fall back to step()
         if not self._in_step:
             self._in_step = True
-            self._step += 1
+            if not self.graph_mode:  # graph mode: begin_graph_step() counts the step
+                self._step += 1
         if self.stream is None:
             if work is not None:
                 work.wait()
@@ -117,7 +147,7 @@ class FlatAdamW(torch.optim.AdamW):
                 loss = closure()
         if self.overlap and self.grad_scale_dev is None:
             self.reducer.finish()  # launches (and so updates) any bucket not yet ready
-            if not self._in_step:  # no bucket fired (no backward this step)
+            if not self._in_step and not self.graph_mode:  # no bucket fired (no backward this step)
                 self._step += 1
             if self.stream is not None:
                 torch.cuda.current_stream(self.flat.data.device).wait_stream(self.stream)
@@ -125,7 +155,8 @@ class FlatAdamW(torch.optim.AdamW):
             self._done_ranges = []
             return loss
         g = self.param_groups[0]
-        self._step += 1
+        if not self.graph_mode:
+            self._step += 1
         b1, b2 = g["betas"]
         lr, eps, wd = float(g["lr"]), float(g["eps"]), float(g["weight_decay"])
         bc1 = 1.0 - b1 ** self._step
@@ -133,7 +164,7 @@ class FlatAdamW(torch.optim.AdamW):
         f = self.flat
         if f.data.is_cuda:
             _ext.require_for(f.data).adamw_flat_(f.data, f.grad, self.exp_avg, self.exp_avg_sq, lr, b1, b2, eps, wd,
-                                                 bc1, bc2_sqrt, self.grad_scale, self.grad_scale_dev)
+                                                 bc1, bc2_sqrt, self.grad_scale, self.grad_scale_dev, self.hyper)
         else:
             self._step_reference(lr, b1, b2, eps, wd, bc1, bc2_sqrt)
         return loss

@@ -121,8 +121,6 @@ def train(args):
     with set_default_dtype(model_dtype), torch.device(device):
         model = Transformer(model_config)
     flat = model.flatten_()
-    if args.compile:
-        log_rank0("--compile: the step already runs fused HIP kernels; Inductor/Triton is not used")
     overlap = not (args.clip_grad or args.no_overlap_optimizer)
     reducer = None
     if is_dist:
@@ -137,6 +135,19 @@ def train(args):
         optimizer.enable_overlap(reducer)
         optimizer.pre_update_fences.append(ckcore.fence_all)
     lr_scheduler = build_lr_scheduler(optimizer, args.lr_warmup_steps)
+    step_graph = None
+    if args.compile:
+        if use_cuda:
+            from .graph import StepGraph
+
+            pre = (lambda: setattr(optimizer, "grad_scale_dev",
+                                   _clip_coef(flat, args.grad_max_norm, 1.0 / world_size))) if args.clip_grad else None
+            step_graph = StepGraph(model, optimizer, reducer, fences=[ckcore.fence_all], pre_step=pre)
+            log_rank0(f"--compile: the training step is captured into a HIP graph after "
+                      f"{args.compile_warmup_steps} eager steps and replayed (no Inductor/Triton)")
+        else:
+            log_rank0("--compile: no GPU, running eagerly")
+    eager_steps_this_run = 0
     num_flop_per_token_ = num_flop_per_token(model.num_params(exclude_embedding=True), model_config)
     log_rank0(f"Model parameters: {model.num_params() / 1e9:.3f} B, FLOPs/token: {num_flop_per_token_ / 1e9:.2f} G")
 
@@ -248,15 +259,19 @@ def train(args):
         input_ids = input_ids.to(device, non_blocking=True)
         labels = labels.to(device, non_blocking=True)
 
-        optimizer.zero_grad()
-        loss = model(input_ids, labels=labels)
-        loss.backward()
-        if reducer is not None:
-            reducer.finish()
-        if args.clip_grad:
-            optimizer.grad_scale_dev = _clip_coef(flat, args.grad_max_norm, 1.0 / world_size)
-        ckcore.fence_all()  # an async snapshot must land before parameters change
-        optimizer.step()
+        if step_graph is not None and eager_steps_this_run >= args.compile_warmup_steps:
+            loss = step_graph.step(input_ids, labels)  # fences the snapshot before the replay
+        else:
+            optimizer.zero_grad()
+            loss = model(input_ids, labels=labels)
+            loss.backward()
+            if reducer is not None:
+                reducer.finish()
+            if args.clip_grad:
+                optimizer.grad_scale_dev = _clip_coef(flat, args.grad_max_norm, 1.0 / world_size)
+            ckcore.fence_all()  # an async snapshot must land before parameters change
+            optimizer.step()
+            eager_steps_this_run += 1
         lr_scheduler.step()
 
         if csv_writer is not None:
