@@ -67,7 +67,7 @@ def main():
         lrank, world = 0, 1
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    dev = torch.device("cuda", lrank)
+    dev = torch.device("cuda", D.gpu_index(lrank))
     torch.cuda.set_device(dev)
     rank = D.get_rank()
 

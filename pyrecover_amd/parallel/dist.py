@@ -67,6 +67,13 @@ def local_rank() -> int:
     return _STATE["local_rank"]
 
 
+def gpu_index(lrank: int) -> int:
+    """GPU of a local rank: one process per GPU. ``PYRECOVER_LOCAL_DEVICE=<i>`` pins every rank to
+    GPU i (rehearsing the multi-rank path on one GPU; use with PYRECOVER_DIST_BACKEND=gloo)."""
+    o = os.environ.get("PYRECOVER_LOCAL_DEVICE")
+    return int(o) if o not in (None, "") else lrank
+
+
 def maybe_init_distributed(activate_distributed: bool, backend: Optional[str] = None,
                            timeout_s: float = 1800.0) -> Tuple[int, int]:
     """Returns (local_rank, world_size). Initializes the process group when a multi-process
@@ -86,13 +93,13 @@ def maybe_init_distributed(activate_distributed: bool, backend: Optional[str] = 
     os.environ.setdefault("MASTER_PORT", "29500")
     use_gpu = torch.cuda.is_available()
     if backend is None:
-        backend = "nccl" if use_gpu else "gloo"  # "nccl" is RCCL on ROCm
+        backend = os.environ.get("PYRECOVER_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")  # nccl = RCCL
     if use_gpu:
-        torch.cuda.set_device(lrank)
+        torch.cuda.set_device(gpu_index(lrank))
     if not torch.distributed.is_initialized():
         kw = {}
         if backend == "nccl":
-            kw["device_id"] = torch.device("cuda", lrank)
+            kw["device_id"] = torch.device("cuda", gpu_index(lrank))
         torch.distributed.init_process_group(backend=backend, rank=rank, world_size=world,
                                              timeout=datetime.timedelta(seconds=timeout_s), **kw)
     _STATE.update(rank=rank, world=world, local_rank=lrank, initialized=True, backend=backend)

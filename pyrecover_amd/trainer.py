@@ -84,7 +84,7 @@ def train(args):
     is_dist = world_size > 1
     log_rank0(f"Experiment args: {args}")
     use_cuda = torch.cuda.is_available()
-    device = torch.device("cuda", local_rank) if use_cuda else torch.device("cpu")
+    device = torch.device("cuda", D.gpu_index(local_rank)) if use_cuda else torch.device("cpu")
     model_dtype = PRECISION_STR_TO_DTYPE[args.model_dtype]
     torch.manual_seed(args.seed)
     random.seed(args.seed)
