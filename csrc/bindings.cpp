@@ -348,6 +348,20 @@ void adamw_flat_(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, 
         "adamw_flat");
 }
 
+// dst = src^T for a 2-D 16-bit tensor (bf16/fp16) with R, C multiples of 64.
+at::Tensor transpose2d(const at::Tensor& src) {
+  const Range range_("pyrecover::transpose2d");
+  check_dev(src, "src");
+  check_row_major(src, "src");
+  TORCH_CHECK(src.element_size() == 2, "transpose2d: 16-bit dtype required");
+  const int64_t R = src.size(0), C = src.size(1);
+  TORCH_CHECK(R % 64 == 0 && C % 64 == 0 && src.stride(0) % 8 == 0, "transpose2d: R, C must be multiples of 64");
+  const c10::DeviceGuard guard(src.device());
+  at::Tensor dst = at::empty({C, R}, src.options());
+  check(pra_transpose16(src.data_ptr(), dst.data_ptr(), R, C, src.stride(0), R, stream_of(src)), "transpose2d");
+  return dst;
+}
+
 // returns fp32 [2] = {norm, clip_coef}
 at::Tensor grad_norm(const at::Tensor& x, double max_norm, double pre_scale) {
   const Range range_("pyrecover::grad_norm");
@@ -447,6 +461,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("bc1"), py::arg("bc2_sqrt"),
         py::arg("gscale"), py::arg("gscale_dev") = py::none(), py::arg("hyper_dev") = py::none());
   m.def("grad_norm", &grad_norm);
+  m.def("transpose2d", &transpose2d);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   register_ckpt_engine(m);

@@ -146,6 +146,35 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const int64_t* __restric
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// 2-D transpose of a 16-bit [R, C] matrix into [C, R] (64x64 tiles through LDS, 16-B loads and
+// stores on both sides). Used to hand hipBLASLt the weight-gradient GEMM in its fast K-contiguous
+// ("TN") layout: dW = dY^T X computed as dYt (Xt)^T with dYt = [out, T], Xt = [in, T].
+// Requires R % 64 == 0, C % 64 == 0, 16-B aligned rows (host-checked).
+template <typename T>
+__global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ src, T* __restrict__ dst, long ld_src,
+                                                        long ld_dst) {
+  __shared__ __attribute__((aligned(16))) uint16_t tile[64][72];  // +8 pad: 16-B rows, fewer conflicts
+  const long r0 = (long)blockIdx.y * 64, c0 = (long)blockIdx.x * 64;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = t + 256 * i, r = idx >> 3, ch = idx & 7;
+    *reinterpret_cast<uint4*>(&tile[r][ch * 8]) =
+        *reinterpret_cast<const uint4*>(src + (r0 + r) * ld_src + c0 + ch * 8);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = t + 256 * i, rg = idx & 7, c = idx >> 3;  // 8 lanes write one 128-B output row piece
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      w[j] = (uint32_t)tile[rg * 8 + 2 * j][c] | ((uint32_t)tile[rg * 8 + 2 * j + 1][c] << 16);
+    *reinterpret_cast<uint4*>(dst + (c0 + c) * ld_dst + r0 + rg * 8) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 }  // namespace pra
 
 extern "C" {
@@ -198,6 +227,14 @@ hipError_t pra_embedding_bwd(int dtype, const int64_t* sorted_ids, const int64_t
   PRA_DISPATCH_FLOAT(dtype, T,
                      hipLaunchKernelGGL((pra::embed_bwd_kernel<T>), dim3(grid), dim3(256), 0, s, sorted_ids, perm,
                                         (const T*)dout, (T*)dW, ntok, D, V, accumulate));
+  return hipGetLastError();
+}
+
+hipError_t pra_transpose16(const void* src, void* dst, long R, long C, long ld_src, long ld_dst, hipStream_t s) {
+  if (R % 64 || C % 64 || ld_src % 8 || ld_dst % 8) return hipErrorInvalidValue;
+  dim3 grid((unsigned)(C / 64), (unsigned)(R / 64));
+  hipLaunchKernelGGL((pra::transpose_kernel<uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)src, (uint16_t*)dst,
+                     ld_src, ld_dst);
   return hipGetLastError();
 }
 

@@ -17,6 +17,7 @@ causal SDPA with GQA, output projection), FeedForward.forward (:268-269), the ou
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional, Sequence, Tuple
 
 import torch
@@ -73,6 +74,27 @@ class FlatSlotAdapter:
 
 def _mm_into(slot, a, b, shape):
     slot.mm_(a, b, shape)
+
+
+# Weight gradients dW = dY^T X with K = tokens. hipBLASLt runs this GEMM ~25-30% faster when both
+# operands are K-contiguous ("TN": dYt [out, T] times Xt [in, T]^T) than on the row-major
+# activations, which is worth two bandwidth-bound HIP transposes for the large projections
+# (QKV, W1|W3, output head; tools/gemm_bench.py --layouts). PYRECOVER_TN_WGRAD=0 disables it.
+TN_WGRAD = os.environ.get("PYRECOVER_TN_WGRAD", "1") == "1"
+
+
+def _tn_ok(t):
+    return (t.is_cuda and t.dim() == 2 and t.element_size() == 2 and t.stride(1) == 1 and t.size(0) % 64 == 0
+            and t.size(1) % 64 == 0 and t.stride(0) % 8 == 0)
+
+
+def _wgrad_into(slot, dy2, x2, shape):
+    """slot <- dy2^T x2 (dy2 [T, out], x2 [T, in])."""
+    if TN_WGRAD and _tn_ok(dy2) and _tn_ok(x2):
+        C = _ext.require_for(dy2)
+        slot.mm_(C.transpose2d(dy2), C.transpose2d(x2).t(), shape)
+    else:
+        slot.mm_(dy2.t(), x2, shape)
 
 
 # ---------------------------------------------------------------------------------------
@@ -284,7 +306,7 @@ class _AttentionBlock(torch.autograd.Function):
         else:
             ref.rope_inplace_2d(dqkv, nq + nk, tab, D, S, inverse=True)
         dx = torch.mm(dqkv, w_qkv)
-        slot_qkv.mm_(dqkv.t(), x2, tuple(w_qkv.shape))
+        _wgrad_into(slot_qkv, dqkv, x2, tuple(w_qkv.shape))
         n_params = ctx.needs_input_grad.__len__() - 7
         return (dx.view(B, S, -1), None, None, None, None, None, None) + (None,) * n_params
 
@@ -336,7 +358,7 @@ class _SwiGLUMLP(torch.autograd.Function):
         slot2.mm_(dy2.t(), a, tuple(w2.shape))
         dgu = _swiglu_bwd_(da, gu)  # in place over gu (dead after this)
         dx = torch.mm(dgu, w13)
-        slot13.mm_(dgu.t(), x2, tuple(w13.shape))
+        _wgrad_into(slot13, dgu, x2, tuple(w13.shape))
         n_params = len(ctx.needs_input_grad) - 5
         return (dx.view(shape), None, None, None, None) + (None,) * n_params
 
@@ -384,7 +406,7 @@ class _LinearCrossEntropy(torch.autograd.Function):
             p = p * valid.float().unsqueeze(1) * (dloss.float() / n)
             dlogits = p.to(logits.dtype)
         dh = torch.mm(dlogits, w_out)
-        ctx.slot.mm_(dlogits.t(), h2, tuple(w_out.shape))
+        _wgrad_into(ctx.slot, dlogits, h2, tuple(w_out.shape))
         return dh.view(ctx.hshape), None, None, None, None, None
 
 

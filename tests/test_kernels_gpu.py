@@ -245,3 +245,12 @@ def test_single_hip_runtime_loaded(cuda):
     maps = open("/proc/self/maps").read()
     libs = {line.split()[-1] for line in maps.splitlines() if "libamdhip64" in line}
     assert len(libs) == 1, libs
+
+
+@pytest.mark.parametrize("R,C", [(64, 64), (256, 192), (2048, 1024), (128, 32000)])
+def test_transpose2d_exact(cuda, R, C):
+    C_ = _ext.native()
+    x = torch.randn(R, C, device=cuda).bfloat16()
+    assert torch.equal(C_.transpose2d(x), x.t().contiguous())
+    xs = torch.randn(R, C + 64, device=cuda).bfloat16()[:, 64:]  # strided rows
+    assert torch.equal(C_.transpose2d(xs), xs.t().contiguous())

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--vocab", type=int, default=32000)
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--no-table", action="store_true")
+    ap.add_argument("--layouts", action="store_true", help="also time K-contiguous wgrad / transpose variants")
     a = ap.parse_args()
     from pyrecover_amd.utils.gemm_tuning import configure_gemm_tuning
 
@@ -37,6 +38,11 @@ def main():
         dy = torch.randn(T, n_out, device=dev).bfloat16()
         cases = {"fwd": lambda: torch.mm(x, w.t()), "dgrad": lambda: torch.mm(dy, w),
                  "wgrad": lambda: torch.mm(dy.t(), x)}
+        if a.layouts:  # K-contiguous (transposed) activations: wgrad as a "TN" GEMM
+            dyT, xT = dy.t().contiguous(), x.t().contiguous()
+            cases.update({"wgrad_tn": lambda: torch.mm(dyT, xT.t()), "wgrad_dyT_x": lambda: torch.mm(dyT, x),
+                          "dgrad_from_dyT": lambda: torch.mm(dyT.t(), w),
+                          "transpose_dy": lambda: dy.t().contiguous(), "transpose_x": lambda: x.t().contiguous()})
         for cname, fn in cases.items():
             for _ in range(3):
                 fn()
@@ -50,8 +56,9 @@ def main():
             ms = e0.elapsed_time(e1) / a.iters
             res[f"{name}_{cname}"] = {"ms": round(ms, 4), "tflops": round(2 * T * n_in * n_out / ms / 1e9, 1)}
         del x, w, dy
-    tot_ms = sum(v["ms"] for k, v in res.items() if not k.startswith("head")) * 32 + sum(
-        v["ms"] for k, v in res.items() if k.startswith("head"))
+    base = [k for k in res if k.split("_", 1)[1] in ("fwd", "dgrad", "wgrad")]
+    tot_ms = sum(res[k]["ms"] for k in base if not k.startswith("head")) * 32 + sum(
+        res[k]["ms"] for k in base if k.startswith("head"))
     print(json.dumps({"table": not a.no_table, "gemm_ms_per_step": round(tot_ms, 1), "shapes": res}), flush=True)
 
 
