@@ -241,6 +241,46 @@ at::Tensor swiglu_bwd(const at::Tensor& dy, const at::Tensor& gu, c10::optional<
   return dgu;
 }
 
+// In place: gu <- [dg | du] (the SwiGLU backward, same math as swiglu_bwd); returns dgu^T [2F, T].
+at::Tensor swiglu_bwd_t_(const at::Tensor& dy, at::Tensor gu) {
+  const Range range_("pyrecover::swiglu_bwd_t");
+  check_dev(gu, "gu");
+  check_row_major(gu, "gu");
+  check_row_major(dy, "dy");
+  const int64_t T = gu.size(0), F = gu.size(1) / 2;
+  TORCH_CHECK(gu.element_size() == 2, "swiglu_bwd_t: 16-bit dtype required");
+  TORCH_CHECK(dy.size(0) == T && dy.size(1) == F && dy.scalar_type() == gu.scalar_type(), "swiglu_bwd_t: dy");
+  TORCH_CHECK(T % 64 == 0 && F % 64 == 0, "swiglu_bwd_t: tokens and F must be multiples of 64");
+  same_dev(gu, dy, "dy");
+  const c10::DeviceGuard guard(gu.device());
+  at::Tensor guT = at::empty({2 * F, T}, gu.options());
+  check(pra_swiglu_bwd_t(dt(gu), dy.data_ptr(), gu.data_ptr(), guT.data_ptr(), T, (int)F, (int)gu.stride(0),
+                         (int)dy.stride(0), stream_of(gu)),
+        "swiglu_bwd_t");
+  return guT;
+}
+
+// In place RoPE (inverse if requested) on the first `nrot` columns of x2d [T, C]; returns x2d^T.
+at::Tensor rope_t_(at::Tensor x2d, int64_t nrot, const at::Tensor& tab, int64_t head_dim, int64_t seq_len,
+                   bool inverse) {
+  const Range range_("pyrecover::rope_t");
+  check_dev(x2d, "x");
+  check_row_major(x2d, "rope_t x");
+  TORCH_CHECK(x2d.element_size() == 2, "rope_t: 16-bit dtype required");
+  TORCH_CHECK(tab.scalar_type() == at::kFloat && tab.is_contiguous(), "rope_t: table must be contiguous fp32");
+  same_dev(x2d, tab, "rope table");
+  TORCH_CHECK(tab.numel() >= seq_len * head_dim, "rope_t: table too small");
+  const int64_t T = x2d.size(0), C = x2d.size(1);
+  TORCH_CHECK(nrot <= C && nrot % head_dim == 0 && head_dim % 8 == 0, "rope_t: bad nrot/head_dim");
+  TORCH_CHECK(T % seq_len == 0 && T % 64 == 0 && C % 64 == 0, "rope_t: shape must tile by 64");
+  const c10::DeviceGuard guard(x2d.device());
+  at::Tensor xT = at::empty({C, T}, x2d.options());
+  check(pra_rope_t(dt(x2d), x2d.data_ptr(), xT.data_ptr(), tab.data_ptr(), T, (int)x2d.stride(0), (int)C, (int)nrot,
+                   (int)head_dim, (int)seq_len, inverse ? 1 : 0, stream_of(x2d)),
+        "rope_t");
+  return xT;
+}
+
 at::Tensor embedding_fwd(const at::Tensor& ids, const at::Tensor& W) {
   const Range range_("pyrecover::embedding_fwd");
   check_dev(W, "W");
@@ -462,6 +502,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("gscale"), py::arg("gscale_dev") = py::none(), py::arg("hyper_dev") = py::none());
   m.def("grad_norm", &grad_norm);
   m.def("transpose2d", &transpose2d);
+  m.def("swiglu_bwd_t_", &swiglu_bwd_t_);
+  m.def("rope_t_", &rope_t_);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   register_ckpt_engine(m);

@@ -138,3 +138,11 @@ __device__ __forceinline__ float block_max(float v, float* scratch) {
     case ::pra::kF16: { using T = __half; __VA_ARGS__; break; }    \
     default: return hipErrorInvalidValue;                          \
   }
+
+// bf16 / fp16 only (kernels that pack elements into 16-bit LDS tiles)
+#define PRA_DISPATCH_16BIT(dtype, T, ...)                          \
+  switch (dtype) {                                                 \
+    case ::pra::kBF16: { using T = __bf16; __VA_ARGS__; break; }   \
+    case ::pra::kF16: { using T = __half; __VA_ARGS__; break; }    \
+    default: return hipErrorInvalidValue;                          \
+  }

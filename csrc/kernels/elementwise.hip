@@ -175,6 +175,103 @@ __global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ sr
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Transposing epilogues. The weight-gradient GEMM wants dY^T (K = tokens contiguous, see
+// transpose_kernel); the two producers of the largest dY's write it directly, in the same pass
+// that writes the row-major result (needed by the data-gradient GEMM):
+//   swiglu_bwd_t: dgu = [dg | du] (in place over gu) and dguT = dgu^T        (W1|W3 weight grad)
+//   rope_t:       x = inverse-RoPE(x) on the q|k columns (in place), xT = x^T (QKV weight grad)
+// Block = 64 tokens x 64 columns; values go through an LDS tile to 16-B transposed stores.
+__device__ __forceinline__ void store_tile_t(uint16_t (*tile)[72], uint16_t* dst, long ld_dst, long c0, long t0) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = threadIdx.x + 256 * i, rg = idx & 7, c = idx >> 3;
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      w[j] = (uint32_t)tile[rg * 8 + 2 * j][c] | ((uint32_t)tile[rg * 8 + 2 * j + 1][c] << 16);
+    *reinterpret_cast<uint4*>(dst + (c0 + c) * ld_dst + t0 + rg * 8) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void put8(uint16_t* row, const float* v) {
+  T tmp[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) tmp[j] = from_f<T>(v[j]);
+  *reinterpret_cast<uint4*>(row) = *reinterpret_cast<const uint4*>(tmp);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(const T* __restrict__ dy, T* gu, T* __restrict__ guT,
+                                                           int F, int ldgu, int lddy, long ntok) {
+  __shared__ __attribute__((aligned(16))) uint16_t tg[64][72], tu[64][72];
+  const long t0 = (long)blockIdx.y * 64;
+  const int c0 = blockIdx.x * 64;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = threadIdx.x + 256 * i, r = idx >> 3, ch = idx & 7;
+    const long t = t0 + r;
+    const int col = c0 + ch * 8;
+    float gv[8], uv[8], dv[8], og[8], ou[8];
+    load8<T>(gu + t * ldgu + col, gv);
+    load8<T>(gu + t * ldgu + F + col, uv);
+    load8<T>(dy + t * lddy + col, dv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {  // identical math / rounding to swiglu_bwd_kernel
+      const float sg = 1.f / (1.f + __expf(-gv[j]));
+      const float a = rnd<T>(gv[j] * sg);
+      const float da = rnd<T>(dv[j] * uv[j]);
+      ou[j] = dv[j] * a;
+      og[j] = da * sg * (1.f + gv[j] * (1.f - sg));
+    }
+    store8<T>(gu + t * ldgu + col, og);
+    store8<T>(gu + t * ldgu + F + col, ou);
+    put8<T>(&tg[r][ch * 8], og);
+    put8<T>(&tu[r][ch * 8], ou);
+  }
+  __syncthreads();
+  store_tile_t(tg, reinterpret_cast<uint16_t*>(guT), ntok, c0, t0);
+  store_tile_t(tu, reinterpret_cast<uint16_t*>(guT), ntok, F + c0, t0);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void rope_t_kernel(T* x, T* __restrict__ xT, const float2* __restrict__ tab,
+                                                     int ld, int nrot, int D, int S, float sign, long ntok) {
+  __shared__ __attribute__((aligned(16))) uint16_t tile[64][72];
+  const long t0 = (long)blockIdx.y * 64;
+  const int c0 = blockIdx.x * 64;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = threadIdx.x + 256 * i, r = idx >> 3, ch = idx & 7;
+    const long t = t0 + r;
+    const int col = c0 + ch * 8;
+    T* p = x + t * ld + col;
+    float v[8];
+    load8<T>(p, v);
+    if (col < nrot) {  // same math as rope_kernel
+      const int pos = (int)(t % S);
+      const int pi = (col % D) / 2;
+      const float4* tp = reinterpret_cast<const float4*>(tab + (size_t)pos * (D / 2) + pi);
+      const float4 cs01 = tp[0], cs23 = tp[1];
+      const float c[4] = {cs01.x, cs01.z, cs23.x, cs23.z};
+      const float sn[4] = {cs01.y * sign, cs01.w * sign, cs23.y * sign, cs23.w * sign};
+      float o[8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        o[2 * k] = v[2 * k] * c[k] - v[2 * k + 1] * sn[k];
+        o[2 * k + 1] = v[2 * k] * sn[k] + v[2 * k + 1] * c[k];
+      }
+      store8<T>(p, o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = o[j];
+    }
+    put8<T>(&tile[r][ch * 8], v);
+  }
+  __syncthreads();
+  store_tile_t(tile, reinterpret_cast<uint16_t*>(xT), ntok, c0, t0);
+}
+
 }  // namespace pra
 
 extern "C" {
@@ -235,6 +332,28 @@ hipError_t pra_transpose16(const void* src, void* dst, long R, long C, long ld_s
   dim3 grid((unsigned)(C / 64), (unsigned)(R / 64));
   hipLaunchKernelGGL((pra::transpose_kernel<uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)src, (uint16_t*)dst,
                      ld_src, ld_dst);
+  return hipGetLastError();
+}
+
+// dgu = [dg | du] in place over gu [ntok, 2F] (ld ldgu) and guT [2F, ntok]; ntok, F multiples of 64.
+hipError_t pra_swiglu_bwd_t(int dtype, const void* dy, void* gu, void* guT, long ntok, int F, int ldgu, int lddy,
+                            hipStream_t s) {
+  if (ntok % 64 || F % 64 || ldgu % 8 || lddy % 8) return hipErrorInvalidValue;
+  dim3 grid((unsigned)(F / 64), (unsigned)(ntok / 64));
+  PRA_DISPATCH_16BIT(dtype, T,
+                     hipLaunchKernelGGL((pra::swiglu_bwd_t_kernel<T>), grid, dim3(256), 0, s, (const T*)dy, (T*)gu,
+                                        (T*)guT, F, ldgu, lddy, ntok));
+  return hipGetLastError();
+}
+
+// x [ntok, ncols] (ld): RoPE (inverse if `inverse`) on columns [0, nrot), in place; xT = x^T.
+hipError_t pra_rope_t(int dtype, void* x, void* xT, const void* tab, long ntok, int ld, int ncols, int nrot, int D,
+                      int S, int inverse, hipStream_t s) {
+  if (ntok % 64 || ncols % 64 || nrot % 8 || D % 8 || ld % 8) return hipErrorInvalidValue;
+  dim3 grid((unsigned)(ncols / 64), (unsigned)(ntok / 64));
+  PRA_DISPATCH_16BIT(dtype, T,
+                     hipLaunchKernelGGL((pra::rope_t_kernel<T>), grid, dim3(256), 0, s, (T*)x, (T*)xT,
+                                        (const float2*)tab, ld, nrot, D, S, inverse ? -1.f : 1.f, ntok));
   return hipGetLastError();
 }
 

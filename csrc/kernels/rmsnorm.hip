@@ -372,7 +372,9 @@ extern "C" {
 // Number of fp32 workspace rows (each D floats) the backward needs for `rows` rows.
 // Blocks of the backward kernel (= fp32 partial rows of dw); the workspace must hold
 // pra_rmsnorm_bwd_ws_rows(rows) + 4 rows of D floats.
-int pra_rmsnorm_bwd_ws_rows(int rows) { return rows < 256 ? rows : 256; }
+// 1024 blocks = 4 per CU: each block walks its rows one at a time (load -> block reduce -> store),
+// so several blocks per CU are what keeps enough HBM requests in flight.
+int pra_rmsnorm_bwd_ws_rows(int rows) { return rows < 1024 ? rows : 1024; }
 
 hipError_t pra_rmsnorm_fwd(int dtype, const void* x, const void* delta, const void* w, void* h_out,
                            void* y, float* rstd, int rows, int D, float eps, hipStream_t s) {

@@ -301,12 +301,19 @@ class _AttentionBlock(torch.autograd.Function):
         dk = dqkv[:, nq:nq + nk].view(B, S, Hkv, D)
         dv = dqkv[:, nq + nk:].view(B, S, Hkv, D)
         _attn_bwd(q, k, v, o, do, lse, dq, dk, dv, ctx.scale, causal)
-        if dqkv.is_cuda:
-            _ext.require_for(dqkv).rope_(dqkv, nq + nk, tab, D, S, 0, True)
+        if TN_WGRAD and _tn_ok(dqkv) and _tn_ok(x2) and T % S == 0:
+            # inverse RoPE in place + dqkv^T in one pass, for the K-contiguous weight-grad GEMM
+            C = _ext.require_for(dqkv)
+            dqkvT = C.rope_t_(dqkv, nq + nk, tab, D, S, True)
+            dx = torch.mm(dqkv, w_qkv)
+            slot_qkv.mm_(dqkvT, C.transpose2d(x2).t(), tuple(w_qkv.shape))
         else:
-            ref.rope_inplace_2d(dqkv, nq + nk, tab, D, S, inverse=True)
-        dx = torch.mm(dqkv, w_qkv)
-        _wgrad_into(slot_qkv, dqkv, x2, tuple(w_qkv.shape))
+            if dqkv.is_cuda:
+                _ext.require_for(dqkv).rope_(dqkv, nq + nk, tab, D, S, 0, True)
+            else:
+                ref.rope_inplace_2d(dqkv, nq + nk, tab, D, S, inverse=True)
+            dx = torch.mm(dqkv, w_qkv)
+            _wgrad_into(slot_qkv, dqkv, x2, tuple(w_qkv.shape))
         n_params = ctx.needs_input_grad.__len__() - 7
         return (dx.view(B, S, -1), None, None, None, None, None, None) + (None,) * n_params
 
@@ -356,9 +363,16 @@ class _SwiGLUMLP(torch.autograd.Function):
         dy2 = dy.reshape(-1, shape[-1])
         da = torch.mm(dy2, w2)
         slot2.mm_(dy2.t(), a, tuple(w2.shape))
-        dgu = _swiglu_bwd_(da, gu)  # in place over gu (dead after this)
-        dx = torch.mm(dgu, w13)
-        _wgrad_into(slot13, dgu, x2, tuple(w13.shape))
+        if TN_WGRAD and _tn_ok(gu) and _tn_ok(x2) and _tn_ok(da):
+            # SwiGLU backward in place over gu, writing dgu^T in the same pass
+            C = _ext.require_for(gu)
+            dguT = C.swiglu_bwd_t_(da, gu)
+            dx = torch.mm(gu, w13)
+            slot13.mm_(dguT, C.transpose2d(x2).t(), tuple(w13.shape))
+        else:
+            dgu = _swiglu_bwd_(da, gu)  # in place over gu (dead after this)
+            dx = torch.mm(dgu, w13)
+            _wgrad_into(slot13, dgu, x2, tuple(w13.shape))
         n_params = len(ctx.needs_input_grad) - 5
         return (dx.view(shape), None, None, None, None) + (None,) * n_params
 

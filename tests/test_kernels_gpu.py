@@ -254,3 +254,30 @@ def test_transpose2d_exact(cuda, R, C):
     assert torch.equal(C_.transpose2d(x), x.t().contiguous())
     xs = torch.randn(R, C + 64, device=cuda).bfloat16()[:, 64:]  # strided rows
     assert torch.equal(C_.transpose2d(xs), xs.t().contiguous())
+
+
+def test_swiglu_bwd_t_matches_swiglu_bwd_exactly(cuda):
+    C_ = _ext.native()
+    T, F = 256, 192
+    gu = torch.randn(T, 2 * F, device=cuda).bfloat16()
+    dy = torch.randn(T, F, device=cuda).bfloat16()
+    ref = C_.swiglu_bwd(dy, gu.clone(), None)
+    g2 = gu.clone()
+    guT = C_.swiglu_bwd_t_(dy, g2)
+    assert torch.equal(g2, ref)
+    assert torch.equal(guT, ref.t().contiguous())
+
+
+def test_rope_t_matches_rope_exactly(cuda):
+    from pyrecover_amd.ops.reference import precompute_freqs_cis, rope_table
+
+    C_ = _ext.native()
+    B, S, Hq, Hkv, D = 2, 128, 4, 2, 64
+    tab = rope_table(precompute_freqs_cis(D, S, 10000.0)).to(cuda)
+    x = torch.randn(B * S, (Hq + 2 * Hkv) * D, device=cuda).bfloat16()
+    ref = x.clone()
+    C_.rope_(ref, (Hq + Hkv) * D, tab, D, S, 0, True)
+    x2 = x.clone()
+    xT = C_.rope_t_(x2, (Hq + Hkv) * D, tab, D, S, True)
+    assert torch.equal(x2, ref)
+    assert torch.equal(xT, ref.t().contiguous())
