@@ -25,6 +25,8 @@
 // bwd 0.645 ms (530 TF at the 2.5x-forward convention); B16 H64/8 non-causal fwd 835 TF.
 #include "common.h"
 
+#include <stdlib.h>
+
 #include <type_traits>
 
 namespace pra {
@@ -85,14 +87,15 @@ __device__ __forceinline__ float half_sum(float x) {
 template <int D, int ROWS, int NT = 256>
 struct Stage {
   static constexpr int CH = D / 8;
-  static constexpr int CPT = ROWS * CH / NT;
-  static_assert(CPT * NT == ROWS * CH, "tile must split evenly over the block");
+  static constexpr int CPT = (ROWS * CH + NT - 1) / NT;
+  static constexpr bool EXACT = CPT * NT == ROWS * CH;  // else the last pass is partial
   uint4 r[CPT];
   __device__ __forceinline__ void load(const __bf16* g, long ld, int row0, int nrows_valid) {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       const int idx = i * NT + threadIdx.x;
       const int row = idx / CH, c = idx % CH;
+      if (!EXACT && idx >= ROWS * CH) continue;
       if (row0 + row < nrows_valid)
         r[i] = *reinterpret_cast<const uint4*>(g + (long)(row0 + row) * ld + c * 8);
       else
@@ -104,6 +107,7 @@ struct Stage {
     for (int i = 0; i < CPT; ++i) {
       const int idx = i * NT + threadIdx.x;
       const int row = idx / CH, c = idx % CH;
+      if (!EXACT && idx >= ROWS * CH) continue;
       *reinterpret_cast<uint4*>(reinterpret_cast<char*>(tile) + lay_byte<D>(row, c)) = r[i];
     }
   }
@@ -113,17 +117,18 @@ struct Stage {
 // writes 1 KiB per wave-instruction linearly (base + 16 B * lane), so each lane fetches the
 // (row, chunk) that the image places at its linear position.
 // No VGPR staging; rows must be in bounds (callers guarantee S % tile == 0).
-template <int D, int ROWS>
+template <int D, int ROWS, int NWV = 4>
 struct GStage {
   static constexpr int CH = D / 8;
-  static constexpr int NI = ROWS * CH / 256;
+  static constexpr int NI = ROWS * CH / (NWV * 64);
+  static_assert(NI * NWV * 64 == ROWS * CH, "tile must split evenly over the block");
   int off[NI];  // element offset of this lane's source chunk relative to the tile's first row
   __device__ __forceinline__ void init(long ld) {
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       int row, ch;
-      lay_inverse<D>(((i * 4 + wid) * 64 + lane) * 16, row, ch);
+      lay_inverse<D>(((i * NWV + wid) * 64 + lane) * 16, row, ch);
       off[i] = row * (int)ld + ch * 8;
     }
   }
@@ -132,7 +137,7 @@ struct GStage {
 #pragma unroll
     for (int i = 0; i < NI; ++i)
       __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(g + off[i]),
-                                       (__attribute__((address_space(3))) void*)(tile + (i * 4 + wid) * 512), 16, 0,
+                                       (__attribute__((address_space(3))) void*)(tile + (i * NWV + wid) * 512), 16, 0,
                                        0);
   }
 };
@@ -350,26 +355,31 @@ __global__ __launch_bounds__(256) void bwd_pre_kernel(const __bf16* __restrict__
 }
 
 // ======================================================================================
-// Backward dK/dV: block = (b, kv head, 128-key tile); wave owns 32 keys. K and V of the block
+// Backward dK/dV: block = (b, kv head, 32*NW-key tile); wave owns 32 keys. K and V of the block
 // stay resident in LDS (read as MFMA operands, so only the dK/dV accumulators live in registers
 // and the kernel fits 2 waves/SIMD); 32-row Q/dO tiles stream through a single LDS buffer,
 // register-staged one tile ahead. Loops over the query heads of the kv head (GQA) and query tiles.
 //   S  = Q K^T   (key on lane)      P  = exp2(S*c - lse*log2e)
 //   dP = dO V^T  (key on lane)      dS = P * (dP - delta)
 //   dV^T += dO^T P                  dK^T += Q^T dS      (accumulators reused as B operands)
-// Per-query constants arrive as one float per lane and are broadcast with ds_bpermute.
+// NW = 8 (256 keys, 144 KB LDS, one 512-thread block per CU): each staged Q/dO tile feeds twice
+// the keys per barrier, and the per-query constants are staged in LDS and read as float4.
+// NW = 4 (128 keys, 80 KB, two blocks per CU): the constants arrive as one float per lane and are
+// broadcast with ds_bpermute (no LDS left for them).
 // ======================================================================================
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(
+template <int D, bool CAUSAL, int NW>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
     const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ V,
     const __bf16* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
     __bf16* __restrict__ dK, __bf16* __restrict__ dV, int S, int Hq, int Hkv, long ldq, long ldk, long ldv,
     long lddo, long lddk, long lddv, float scale, float scale_log2) {
-  constexpr int KB = 128, QT = 32;
+  constexpr int KB = 32 * NW, QT = 32, NT = NW * 64;
   constexpr int NKS = D / 16, NDB = D / 32;
   constexpr int KVT = KB * D, QDT = QT * D;
+  constexpr bool ROWC_LDS = NW == 8;
   // Q and dO first: their (transposed) reads then use 16-bit immediate offsets off one base
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * KVT + 2 * QDT];  // Q dO K V
+  __shared__ __attribute__((aligned(16))) float rowc[ROWC_LDS ? 2 : 1][32];  // lse*log2e | delta
   __bf16* const Qs = smem;
   __bf16* const Ds = smem + QDT;
   __bf16* const Ks = smem + 2 * QDT;
@@ -386,7 +396,7 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(
   const int krow = kw + l32;
 
   {
-    GStage<D, KB> gk, gv;
+    GStage<D, KB, NW> gk, gv;
     gk.init(ldk);
     gv.init(ldv);
     gk.issue(K + ((long)b * S + k0) * ldk + hk * D, Ks);
@@ -410,12 +420,14 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(
   int bp_base = 4 * (4 * h2);  // ds_bpermute byte address of lane crow(0, h2)
   asm volatile("" : "+v"(bp_base));  // opaque: per-row offsets then fold into the ds offset field
 
-  Stage<D, QT> sq, sd;
+  Stage<D, QT, NT> sq, sd;
+  float rc_next = 0.f;
   auto stage_load = [&](int it) {
     const int hq = hk * nrep + it / nqt;
     const int q0 = qstart + (it % nqt) * QT;
     sq.load(Q + (long)b * S * ldq + hq * D, ldq, q0, S);
     sd.load(dO + (long)b * S * lddo + hq * D, lddo, q0, S);
+    if (ROWC_LDS && wid == 0) rc_next = rc_base[(long)hq * S + q0] * rc_mul;
   };
   if (total > 0) stage_load(0);
 
@@ -424,7 +436,12 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(
     const int q0 = qstart + (it % nqt) * QT;
     sq.store(Qs);
     sd.store(Ds);
-    const float rcv = rc_base[(long)hq * S + q0] * rc_mul;
+    float rcv = 0.f;
+    if constexpr (ROWC_LDS) {
+      if (wid == 0) rowc[h2][l32] = rc_next;
+    } else {
+      rcv = rc_base[(long)hq * S + q0] * rc_mul;
+    }
     __syncthreads();
     if (it + 1 < total) stage_load(it + 1);
     if (!(CAUSAL && q0 + QT - 1 < kw)) {
@@ -446,14 +463,29 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(
       }
       const bool diag = CAUSAL && q0 == kw;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int src = bp_base + 4 * ((r & 3) + 8 * (r >> 2));
-        const float lse2 = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(rcv)));
-        const float dl = __int_as_float(__builtin_amdgcn_ds_bpermute(src + 128, __float_as_int(rcv)));
-        float p = fexp2(fmaf(s[r], scale_log2, -lse2));
-        if (diag && l32 > crow(r, h2)) p = 0.f;
-        s[r] = p;
-        dp[r] = p * (dp[r] - dl);
+      for (int rr = 0; rr < 4; ++rr) {
+        float lse4[4], dl4[4];
+        if constexpr (ROWC_LDS) {
+          const float4 a = *reinterpret_cast<const float4*>(&rowc[0][8 * rr + 4 * h2]);
+          const float4 c = *reinterpret_cast<const float4*>(&rowc[1][8 * rr + 4 * h2]);
+          lse4[0] = a.x; lse4[1] = a.y; lse4[2] = a.z; lse4[3] = a.w;
+          dl4[0] = c.x; dl4[1] = c.y; dl4[2] = c.z; dl4[3] = c.w;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int src = bp_base + 4 * (j + 8 * rr);
+            lse4[j] = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(rcv)));
+            dl4[j] = __int_as_float(__builtin_amdgcn_ds_bpermute(src + 128, __float_as_int(rcv)));
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 4 * rr + j;
+          float p = fexp2(fmaf(s[r], scale_log2, -lse4[j]));
+          if (diag && l32 > crow(r, h2)) p = 0.f;
+          s[r] = p;
+          dp[r] = p * (dp[r] - dl4[j]);
+        }
       }
       const bf16x8 p0 = pack8(s, 0), p1 = pack8(s, 1), d0 = pack8(dp, 0), d1 = pack8(dp, 1);
       bf16x8 ot = lo.tr(Ds, 0, 0), qt = lo.tr(Qs, 0, 0);
@@ -667,13 +699,23 @@ hipError_t pra_attn_bwd(const void* q, const void* k, const void* v, const void*
                          (const __bf16*)dout, delta, B, S, Hq, ldo, lddo);
   }
   {
-    dim3 grid((S / 128) * Hkv * B);
-#define LAUNCH(DD, CC)                                                                                         \
-  hipLaunchKernelGGL((bwd_dkdv_kernel<DD, CC>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,     \
-                     (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dk, (__bf16*)dv, S, Hq, Hkv, ldq, \
-                     ldk, ldv, lddo, lddk, lddv, scale, sl2)
-    if (D == 128) { if (causal) LAUNCH(128, true); else LAUNCH(128, false); }
-    else { if (causal) LAUNCH(64, true); else LAUNCH(64, false); }
+    static const int nw_env = [] {
+      const char* e = getenv("PRA_DKDV_NW");
+      return e ? atoi(e) : 0;
+    }();
+    const int nw = (nw_env == 4 || S % 256) ? 4 : 8;
+    dim3 grid((S / (32 * nw)) * Hkv * B);
+#define LAUNCH(DD, CC, NWW)                                                                                     \
+  hipLaunchKernelGGL((bwd_dkdv_kernel<DD, CC, NWW>), grid, dim3(NWW * 64), 0, st, (const __bf16*)q,             \
+                     (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dk, (__bf16*)dv, \
+                     S, Hq, Hkv, ldq, ldk, ldv, lddo, lddk, lddv, scale, sl2)
+    if (nw == 8) {
+      if (D == 128) { if (causal) LAUNCH(128, true, 8); else LAUNCH(128, false, 8); }
+      else { if (causal) LAUNCH(64, true, 8); else LAUNCH(64, false, 8); }
+    } else {
+      if (D == 128) { if (causal) LAUNCH(128, true, 4); else LAUNCH(128, false, 4); }
+      else { if (causal) LAUNCH(64, true, 4); else LAUNCH(64, false, 4); }
+    }
 #undef LAUNCH
   }
   {
