@@ -36,6 +36,8 @@ def parse():
     ap.add_argument("--profile-steps", type=int, default=0, help="emit roctx ranges for this many steps")
     ap.add_argument("--no-overlap-optimizer", action="store_true",
                     help="AdamW after backward instead of per bucket during backward")
+    ap.add_argument("--allreduce", choices=["rccl", "xgmi"], default="rccl",
+                    help="gradient all-reduce: RCCL (default) or the direct per-link xGMI backend")
     ap.add_argument("--graph", action="store_true",
                     help="capture the step into a HIP graph after the warmup steps (train.py --compile)")
     ap.add_argument("--phase-timing", action="store_true",
@@ -81,7 +83,7 @@ def main():
     flat = model.flatten_()
     if world > 1:
         broadcast_flat(flat)
-    reducer = GradReducer(flat, bucket_cap_mb=args.bucket_mb)
+    reducer = GradReducer(flat, bucket_cap_mb=args.bucket_mb, backend=args.allreduce)
     opt = FlatAdamW(flat, lr=args.lr, fused=True, grad_scale=1.0 / world)
     if not args.no_overlap_optimizer:
         opt.enable_overlap(reducer)
@@ -171,7 +173,8 @@ def main():
             "data": "synthetic (uniform random token ids), random-init weights",
             "config": {"model": f"{args.model}-shape ({n_params / 1e9:.2f}B params)", "global_batch": B * world,
                        "seq_len": S, "parallelism": f"dp{world}", "batch_per_gpu": B,
-                       "bucket_mb": args.bucket_mb if world > 1 else None, "optimizer": "AdamW (flat fused HIP)" + ("" if args.no_overlap_optimizer else ", overlapped with backward")},
+                       "bucket_mb": args.bucket_mb if world > 1 else None,
+                       "allreduce": args.allreduce if world > 1 else None, "optimizer": "AdamW (flat fused HIP)" + ("" if args.no_overlap_optimizer else ", overlapped with backward")},
             "tokens_per_sec_per_gpu": round(tps / world, 2),
             "model_tflops_per_gpu": round(fpt * tps / world / 1e12, 2),
             "mfu_pct_vs_2.5PF": round(100 * fpt * tps / world / 2.5e15, 2),

@@ -480,6 +480,7 @@ void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, con
 }  // namespace
 
 void register_ckpt_engine(pybind11::module& m);  // csrc/runtime/ckpt_engine.cpp
+void register_xgmi(pybind11::module& m);         // csrc/dist/xgmi.cpp
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "pyrecover_amd native ops (HIP/gfx950 kernels + checkpoint engine)";
@@ -507,4 +508,5 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   register_ckpt_engine(m);
+  register_xgmi(m);
 }

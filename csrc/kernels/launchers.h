@@ -47,6 +47,8 @@ int pra_sumsq_partials();
 hipError_t pra_grad_norm(int dtype, const void* x, long n, float* ws, float* out, float max_norm, float pre_scale,
                          hipStream_t s);
 
+hipError_t pra_sum_slices(int dtype, const void* const* srcs, int nsrc, void* dst, long n, hipStream_t s);
+
 hipError_t pra_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int Hq,
                         int Hkv, int D, long ldq, long ldk, long ldv, long ldo, float scale, int causal,
                         hipStream_t st);

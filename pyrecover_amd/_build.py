@@ -69,7 +69,8 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:
                                              "-DTORCH_API_INCLUDE_EXTENSION_H", "-DUSE_ROCM=1",
                                              f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-Wno-unused-result"]
     kernels = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
-    hosts = [os.path.join(CSRC, "bindings.cpp")] + sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
+    hosts = [os.path.join(CSRC, "bindings.cpp")] + sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))) + sorted(
+        glob.glob(os.path.join(CSRC, "dist", "*.cpp")))
     hdr_t = _newest_header()
     tasks = []
     objs = []

@@ -87,6 +87,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--num-workers", type=int, default=2, help="DataLoader workers (tokenization off the hot loop)")
     p.add_argument("--bucket-cap-mb", type=float, default=256.0, help="DDP all-reduce bucket size")
+    p.add_argument("--allreduce", choices=["rccl", "xgmi"], default="rccl",
+                   help="gradient all-reduce backend: RCCL rings (default) or the direct per-link xGMI "
+                        "reduce-scatter/all-gather over IPC-mapped peer buffers (single node)")
     p.add_argument("--async-checkpoint", action="store_true",
                    help="snapshot to pinned host memory and write in the background while training continues")
     p.add_argument("--no-fsync", action="store_true", help="skip fsync of checkpoint files")

@@ -14,6 +14,8 @@ train.py:107-115 and its Reducer).
 * The gradient is SUM-reduced; the 1/world_size average is folded into the optimizer kernel
   (``FlatAdamW.grad_scale``), so there is no separate scaling pass.
 * Deterministic: identical bucket order/boundaries on every rank and every step.
+* ``backend="xgmi"`` swaps RCCL for the direct per-link all-reduce of
+  :mod:`pyrecover_amd.parallel.xgmi` (same buckets, same hooks).
 * With ``world_size == 1`` (or no process group) the same bucket machinery runs without
   communication, so bucket hooks (the overlapped optimizer) work identically on one GPU.
 * Bucket hooks ``fn(bucket, lo, hi, work)`` run right after a bucket is launched; the
@@ -31,10 +33,14 @@ from .flat import FlatParams
 
 
 class GradReducer:
-    def __init__(self, flat: FlatParams, group=None, bucket_cap_mb: float = 256.0, first_bucket_mb: float = 64.0):
+    def __init__(self, flat: FlatParams, group=None, bucket_cap_mb: float = 256.0, first_bucket_mb: float = 64.0,
+                 backend: str = "rccl"):
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+        if backend not in ("rccl", "xgmi"):
+            raise ValueError(f"unknown all-reduce backend {backend!r}")
+        self.backend = backend if self.world > 1 else "rccl"
         self.hooks = []
         esz = flat.grad.element_size()
         cap = int(bucket_cap_mb * 2 ** 20 / esz)
@@ -68,6 +74,11 @@ class GradReducer:
         self.next_to_launch = 0
         self.enabled = True
         flat.reducer = self
+        self.xgmi = None
+        if self.backend == "xgmi":
+            from .xgmi import XgmiAllReduce
+
+            self.xgmi = XgmiAllReduce(flat, self.ranges, group)
 
     @property
     def num_buckets(self) -> int:
@@ -95,7 +106,9 @@ class GradReducer:
     def _launch(self, b: int):
         lo, hi = self.ranges[b]
         work = None
-        if self.world > 1:
+        if self.xgmi is not None:
+            work = self.xgmi.launch(b)
+        elif self.world > 1:
             work = dist.all_reduce(self.flat.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self.works[b] = work
         for h in self.hooks:
@@ -113,6 +126,8 @@ class GradReducer:
             if w is not None:
                 w.wait()
         self.works = [None] * len(self.counts)
+        if self.xgmi is not None:
+            self.xgmi.end_step()
 
 
 def broadcast_flat(flat: FlatParams, src: int = 0, group=None, chunk_mb: int = 1024):

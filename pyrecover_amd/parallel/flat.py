@@ -130,6 +130,18 @@ class FlatParams:
         return self.slot_of[id(p)]
 
     # --- step protocol ----------------------------------------------------------------
+    def rebind_grad(self, new: torch.Tensor):
+        """Move the gradient space into ``new`` (same numel/dtype/device; e.g. an IPC-exportable
+        allocation for the xGMI all-reduce): every ``p.grad`` and slot view is re-pointed."""
+        if new.numel() != self.numel or new.dtype != self.grad.dtype or new.device != self.grad.device:
+            raise ValueError("rebind_grad: buffer must match the flat gradient buffer")
+        self.grad = new
+        for p in self.params:
+            o = self.param_offset[id(p)]
+            p.grad = new[o:o + p.numel()].view_as(p)
+        for s in self.slots:
+            s.view = new[s.offset:s.offset + s.numel]
+
     def zero_grad(self):
         for s in self.slots:
             s.fresh = True

@@ -1,0 +1,187 @@
+"""Direct intra-node all-reduce over xGMI for the flat gradient buffer.
+
+RCCL's ring moves every byte around the 8 GPUs over one link per direction per ring. On an MI355X
+node every GPU has a direct xGMI link to each of its 7 peers, so this backend works per link
+instead:
+
+* reduce-scatter: rank r owns slice r of each bucket and pulls that slice from all peers at once,
+  one copy per peer on its own HIP stream, so all 7 links are busy;
+* a rank-ordered fp32 reduction kernel (``sum_slices``) sums the slices. The order is fixed and
+  there is one rounding, so every rank gets bit-identical values, deterministically;
+* all-gather: every rank pulls the reduced slices back from their owners, again one stream per peer.
+
+Per bucket, the traffic per link is bucket/W per phase.
+
+Cross-process ordering uses interprocess HIP events only. A peer's copy stream waits, on the GPU,
+on this rank's "bucket ready" / "slice reduced" events, and no kernel spins. The host only
+guarantees that an event was recorded before anyone waits on it. A dedicated comm thread does this
+with two CPU (gloo) barriers per bucket, so the backward thread never blocks.
+
+The gradient buffer is reallocated with ``hipMalloc`` so it can be exported with
+``hipIpcGetMemHandle``. Opt-in: ``GradReducer(..., backend="xgmi")``, ``train.py --allreduce
+xgmi``, ``bench.py --allreduce xgmi``. RCCL stays the default.
+"""
+from __future__ import annotations
+
+import queue
+import threading
+from typing import List, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+from .. import _ext
+
+
+class _Work:
+    __slots__ = ("owner", "b", "ready")
+
+    def __init__(self, owner, b):
+        self.owner = owner
+        self.b = b
+        self.ready = threading.Event()
+
+    def wait(self):
+        """Current stream waits (GPU-side) for the all-reduced bucket."""
+        self.ready.wait()
+        if self.owner.error is not None:
+            raise RuntimeError(f"xgmi all-reduce failed: {self.owner.error}")
+        torch.cuda.current_stream(self.owner.dev).wait_event(self.owner.ev_done[self.b])
+
+
+class XgmiAllReduce:
+    def __init__(self, flat, ranges: Sequence[Tuple[int, int]], group=None):
+        self.C = _ext.native().xgmi
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = W = dist.get_world_size(group)
+        if not 1 < W <= 16:
+            raise ValueError("xgmi all-reduce needs 2..16 ranks on one node")
+        self.flat = flat
+        self.dev = flat.grad.device
+        di = self.dev.index
+        self.dtype = flat.grad.dtype
+        self.esz = flat.grad.element_size()
+        # 1) exportable gradient buffer
+        buf = self.C.ipc_empty(flat.grad.numel(), self.dtype, di)
+        buf.copy_(flat.grad)
+        flat.rebind_grad(buf)
+        self.buf = buf
+        # 2) CPU barriers for the comm thread (its own gloo group, used by nothing else)
+        self.hgroup = dist.new_group(backend="gloo")
+        # 3) peer buffers
+        handles: List = [None] * W
+        dist.all_gather_object(handles, self.C.ipc_mem_handle(buf), group=self.hgroup)
+        base = buf.data_ptr()
+        self.peer_base = [base if r == self.rank else self.C.ipc_open_mem(handles[r], di) for r in range(W)]
+        # 4) slices (identical on every rank; 8-element = 16-B aligned boundaries)
+        self.ranges = list(ranges)
+        self.slices = []
+        for lo, hi in self.ranges:
+            n = hi - lo
+            cuts = [lo + ((n * r // W) // 8) * 8 for r in range(W)] + [hi]
+            self.slices.append([(cuts[r], cuts[r + 1]) for r in range(W)])
+        max_slice = max((s1 - s0) for sl in self.slices for s0, s1 in sl)
+        self.stride = ((max_slice + 63) // 64) * 64
+        self.staging = torch.empty(max(1, (W - 1) * self.stride), dtype=self.dtype, device=self.dev)
+        # 5) events: per bucket "ready" and "reduced" (interprocess), one per-step "done"
+        nb = len(self.ranges)
+        self.ev_ready = [self.C.ipc_event_create(di) for _ in range(nb)]
+        self.ev_rs = [self.C.ipc_event_create(di) for _ in range(nb)]
+        self.ev_step = self.C.ipc_event_create(di)
+        mine = ([self.C.ipc_event_handle(e) for e in self.ev_ready], [self.C.ipc_event_handle(e) for e in self.ev_rs],
+                self.C.ipc_event_handle(self.ev_step))
+        allh: List = [None] * W
+        dist.all_gather_object(allh, mine, group=self.hgroup)
+        self.peer_ready, self.peer_rs, self.peer_step = [], [], []
+        for r in range(W):
+            if r == self.rank:
+                self.peer_ready.append(self.ev_ready)
+                self.peer_rs.append(self.ev_rs)
+                self.peer_step.append(self.ev_step)
+            else:
+                self.peer_ready.append([self.C.ipc_event_open(h, di) for h in allh[r][0]])
+                self.peer_rs.append([self.C.ipc_event_open(h, di) for h in allh[r][1]])
+                self.peer_step.append(self.C.ipc_event_open(allh[r][2], di))
+        self.ev_done = [torch.cuda.Event() for _ in range(nb)]
+        self.ev_sum = torch.cuda.Event()
+        # 6) streams: one per peer (parallel links) + the reduction stream
+        self.comm = torch.cuda.Stream(device=self.dev)
+        self.copy = {r: torch.cuda.Stream(device=self.dev) for r in range(W) if r != self.rank}
+        # 7) comm thread
+        self.q: "queue.Queue" = queue.Queue()
+        self.error = None
+        self.works: List[_Work] = []
+        self.th = threading.Thread(target=self._loop, name="pyrecover-xgmi", daemon=True)
+        self.th.start()
+        dist.barrier(group=self.hgroup)
+
+    # --- backward thread -----------------------------------------------------------------
+    def launch(self, b: int) -> _Work:
+        self.C.event_record(self.ev_ready[b], torch.cuda.current_stream(self.dev).cuda_stream)
+        w = _Work(self, b)
+        self.q.put((b, w))
+        return w
+
+    def end_step(self):
+        """After every bucket of the step was waited on: no rank may overwrite its gradient
+        buffer (next backward) before every peer finished reading it."""
+        done = threading.Event()
+        self.q.put(("step", done))
+        done.wait()
+        if self.error is not None:
+            raise RuntimeError(f"xgmi all-reduce failed: {self.error}")
+        cur = torch.cuda.current_stream(self.dev).cuda_stream
+        for r in range(self.world):
+            if r != self.rank:
+                self.C.stream_wait_event(cur, self.peer_step[r])
+
+    # --- comm thread ---------------------------------------------------------------------
+    def _loop(self):
+        torch.cuda.set_device(self.dev)
+        while True:
+            b, w = self.q.get()
+            try:
+                if b == "step":
+                    self.C.event_record(self.ev_step, self.comm.cuda_stream)
+                    dist.barrier(group=self.hgroup)
+                else:
+                    self._bucket(b)
+            except Exception as e:  # surfaced by the waiter
+                self.error = repr(e)
+            w.set() if b == "step" else w.ready.set()
+
+    def _stage(self, r):
+        k = r if r < self.rank else r - 1
+        return self.staging.data_ptr() + k * self.stride * self.esz
+
+    def _bucket(self, b):
+        C, me, es = self.C, self.rank, self.esz
+        sl = self.slices[b]
+        s0, s1 = sl[me]
+        n = s1 - s0
+        dist.barrier(group=self.hgroup)  # every rank recorded ev_ready[b]
+        # reduce-scatter: pull my slice from every peer, all links at once
+        for r, cs in self.copy.items():
+            h = cs.cuda_stream
+            C.stream_wait_event(h, self.peer_ready[r][b])
+            cs.wait_event(self.ev_sum)  # staging reused: previous bucket's reduction consumed it
+            C.copy_async(self._stage(r), self.peer_base[r] + s0 * es, n * es, h)
+        comm = self.comm
+        C.stream_wait_event(comm.cuda_stream, self.ev_ready[b])
+        for cs in self.copy.values():
+            comm.wait_stream(cs)
+        srcs = [(self.peer_base[me] + s0 * es) if r == me else self._stage(r) for r in range(self.world)]
+        C.sum_slices(srcs, self.peer_base[me] + s0 * es, n, self.dtype, comm.cuda_stream)
+        self.ev_sum.record(comm)
+        C.event_record(self.ev_rs[b], comm.cuda_stream)
+        dist.barrier(group=self.hgroup)  # every rank recorded ev_rs[b]
+        # all-gather: pull each owner's reduced slice into my buffer
+        for r, cs in self.copy.items():
+            h = cs.cuda_stream
+            C.stream_wait_event(h, self.peer_rs[r][b])
+            p0, p1 = sl[r]
+            C.copy_async(self.peer_base[me] + p0 * es, self.peer_base[r] + p0 * es, (p1 - p0) * es, h)
+        for cs in self.copy.values():
+            comm.wait_stream(cs)
+        self.ev_done[b].record(comm)

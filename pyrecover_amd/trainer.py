@@ -126,7 +126,7 @@ def train(args):
     if is_dist:
         broadcast_flat(flat)
     if is_dist or overlap:
-        reducer = GradReducer(flat, bucket_cap_mb=args.bucket_cap_mb)
+        reducer = GradReducer(flat, bucket_cap_mb=args.bucket_cap_mb, backend=args.allreduce)
         log_rank0(f"Gradient buckets: {reducer.num_buckets}, {sum(reducer.bucket_bytes()) / 2**30:.2f} GiB"
                   f"{' (RCCL all-reduce)' if is_dist else ''}")
     model.train()

@@ -19,3 +19,6 @@ timeout -k 10 300 $R --master-port 29514 $T --checkpoint-dir gpurun_out/dist/b -
   > gpurun_out/dist/b2.log 2>&1 || { tail -30 gpurun_out/dist/b2.log; exit 1; }
 timeout -k 10 120 python tools/check_weights_equality.py gpurun_out/dist/a/default-exp/ckpt_6 \
   gpurun_out/dist/b/default-exp/ckpt_6 --distributed --optimizer --tolerance 0
+timeout -k 10 300 $R --master-port 29515 bench.py --gpus 2 --model gpt2-small --batch-per-gpu 2 --steps 4 --warmup 2 \
+  --allreduce xgmi > gpurun_out/dist/bench2_xgmi.log 2>&1 || { tail -30 gpurun_out/dist/bench2_xgmi.log; exit 1; }
+grep '"metric"' gpurun_out/dist/bench2_xgmi.log
