@@ -519,10 +519,18 @@ class CkptEngine {
     std::unique_ptr<Md5Pipe> md5;
     if (want_md5) md5 = std::make_unique<Md5Pipe>();
     uint64_t off = 0;
+    // Fault-injection hook (recovery tests): PYRECOVER_FAULT_HOLD_WRITE=<substring> parks the
+    // writer after the first bytes of a matching archive, so a kill lands mid-write for certain.
+    const char* hold = std::getenv("PYRECOVER_FAULT_HOLD_WRITE");
+    bool hold_now = hold != nullptr && hold[0] != 0 && path.find(hold) != std::string::npos;
     auto emit_copy = [&](const std::vector<uint8_t>& b) {
       write_all(fd, b.data(), b.size());
       if (md5) md5->push_copy(b.data(), b.size());
       off += b.size();
+      if (hold_now) {
+        hold_now = false;
+        std::this_thread::sleep_for(std::chrono::seconds(120));
+      }
     };
     try {
       for (auto& it : items) {

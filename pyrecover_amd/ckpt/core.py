@@ -199,7 +199,7 @@ class Checkpointer:
         self.wait()
         os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
         self.engine.write_items(str(path), items, md5, fsync)
-        self.pending = Job(self, str(path), keepalive, on_done)
+        self.pending = Job(self, str(path), keepalive, on_done, started=time.perf_counter())
         _maybe_inject_fault("during_write", path)
         return self.pending
 
@@ -212,6 +212,17 @@ class Checkpointer:
             return None
         return job.wait()
 
+    def poll(self):
+        """Collect a finished background write without blocking (records its duration)."""
+        if self.pending is not None and not self.engine.busy():
+            self.wait()
+
+
+# Background-write durations feed the time-aware stop: the FINAL checkpoint is written
+# synchronously (and first drains any in-flight write), so the stop threshold must budget the
+# full write time, not the ~ms an async save stalls training (SURVEY §7.2 step 9).
+WRITE_STATS = {"max_seconds": 0.0}
+
 
 @dataclass
 class Job:
@@ -220,6 +231,7 @@ class Job:
     keepalive: Any
     on_done: Optional[Callable]
     result: Optional[Dict[str, Any]] = None
+    started: float = 0.0
 
     def wait(self) -> Dict[str, Any]:
         if self.result is None:
@@ -227,9 +239,31 @@ class Job:
             self.keepalive = None
             if not self.result["ok"]:
                 raise RuntimeError(f"checkpoint write to {self.path} failed: {self.result['error']}")
+            WRITE_STATS["max_seconds"] = max(WRITE_STATS["max_seconds"], float(self.result.get("seconds", 0.0)))
             if self.on_done is not None:
                 self.on_done(self.result)
         return self.result
+
+
+def poll_all():
+    for c in Checkpointer._instances.values():
+        c.poll()
+
+
+def max_write_seconds() -> float:
+    """Longest completed background archive write (0 if none yet)."""
+    return WRITE_STATS["max_seconds"]
+
+
+def inflight_remaining(estimate: float) -> float:
+    """Seconds the in-flight background writes still need, given an estimate of one full write."""
+    now = time.perf_counter()
+    rem = 0.0
+    for c in Checkpointer._instances.values():
+        j = c.pending
+        if j is not None and j.result is None and c.engine.busy():
+            rem = max(rem, estimate - (now - j.started))
+    return max(rem, 0.0)
 
 
 def wait_all():

@@ -74,6 +74,30 @@ def _profiler_stop():
         pass
 
 
+class _StepTimer:
+    """Completed device-side step durations from events recorded at each step end (polled,
+    never blocking). ``record()`` returns the longest completed step seen since the last call."""
+
+    def __init__(self, enabled: bool):
+        self.enabled = enabled
+        self.events = []
+        self.last = None
+
+    def record(self) -> float:
+        if not self.enabled:
+            return 0.0
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        self.events.append(ev)
+        longest = 0.0
+        while self.events and self.events[0].query():
+            e = self.events.pop(0)
+            if self.last is not None:
+                longest = max(longest, self.last.elapsed_time(e) / 1000.0)
+            self.last = e
+        return longest
+
+
 def train(args):
     training_start_time = time.perf_counter()
     total_checkpoint_store_time = 0.0
@@ -148,6 +172,7 @@ def train(args):
         else:
             log_rank0("--compile: no GPU, running eagerly")
     eager_steps_this_run = 0
+    step_timer = _StepTimer(use_cuda)
     num_flop_per_token_ = num_flop_per_token(model.num_params(exclude_embedding=True), model_config)
     log_rank0(f"Model parameters: {model.num_params() / 1e9:.3f} B, FLOPs/token: {num_flop_per_token_ / 1e9:.2f} G")
 
@@ -232,6 +257,14 @@ def train(args):
     loss = None
     while train_step < args.training_steps:
         train_step += 1
+        if stopper is not None:
+            # async saves stall training for ~ms, but the final save is synchronous and first
+            # drains the in-flight write: budget full write times
+            ckcore.poll_all()
+            wsec = ckcore.max_write_seconds()
+            if stopper.update_ckpt(wsec):
+                log_rank0(f"Updated max_ckpt_time from background write time: {stopper.max_ckpt:.2f}")
+            stopper.inflight_drain = ckcore.inflight_remaining(stopper.max_ckpt)
         if stopper is not None and D.is_rank0() and stopper.should_stop():
             should_stop = True
             rem = stopper.remaining()
@@ -279,13 +312,15 @@ def train(args):
             csv_file.flush()
 
         if train_step == 1 or train_step % args.logging_frequency == 0:
+            # sync first: the host runs ahead of the GPU, so an unsynchronized clock would count
+            # queued-but-unexecuted steps (the reference reads the clock before its .item())
+            lval = loss.item()
             time_delta = time.perf_counter() - time_last_log
             tps = ntokens_since_last_log / time_delta
             per_gpu = tps / world_size
             mfu = 100 * num_flop_per_token_ * per_gpu / (args.peak_tflops * 1e12)
             tflops = num_flop_per_token_ * per_gpu / 1e12
             training_tps = ntraining_tokens_since_last_log / time_delta
-            lval = loss.item()
             log_rank0(f"Epoch: {epoch} | Step: {train_step} | Loss: {lval:.2f} | Tokens per second: {tps:.2f} | "
                       f"Training tokens per second (%): {100 * training_tps / tps:.2f} | MFU (%): {mfu:.2f} | "
                       f"TFLOPs: {tflops:.2f} | Tokens per second per GPU: {per_gpu:.2f}")
@@ -299,7 +334,9 @@ def train(args):
             time_last_log = time.perf_counter()
 
         if stopper is not None:
-            iter_time = time.perf_counter() - iter_start
+            # device time per step from events (no sync): the host-side span alone under-counts
+            # while the host runs ahead of the GPU
+            iter_time = max(time.perf_counter() - iter_start, step_timer.record())
             if stopper.update_iter(iter_time):
                 log_rank0(f"Updated max_iter_time: {stopper.max_iter}")
             if train_step % args.logging_frequency == 0:

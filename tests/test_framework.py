@@ -188,7 +188,7 @@ def test_kill_during_save_never_corrupts_latest(tmp_path):
     code = ("import sys; sys.path.insert(0, %r); "
             "from tests.test_framework import _tiny_run; _tiny_run(%r, 4, ['--verify-checkpoints'])"
             % (str(ROOT), str(tmp_path)))
-    env = dict(os.environ, PYRECOVER_FAULT="kill_during_write:ckpt_4")
+    env = dict(os.environ, PYRECOVER_FAULT="kill_during_write:ckpt_4", PYRECOVER_FAULT_HOLD_WRITE="ckpt_4")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, timeout=300)
     assert r.returncode == -9, r.stderr.decode()[-2000:]
     from pyrecover_amd.ckpt.core import get_latest_checkpoint
@@ -216,3 +216,32 @@ def test_op_roctx_ranges_toggle():
     C.set_roctx(False)
     assert not C.roctx_enabled()
     C.set_roctx(was)
+
+
+def test_time_aware_budgets_async_write_and_drain(monkeypatch):
+    """The stop threshold covers a full (synchronous) final write plus what an in-flight async
+    write still needs, not just the async stall."""
+    import time as _t
+
+    from pyrecover_amd.ckpt import core as ck
+    from pyrecover_amd.timelimit import TimeAwareStopper
+
+    st = TimeAwareStopper(1.0, 10.0, end_time=_t.time() + 1000)
+    base = st.threshold
+    monkeypatch.setitem(ck.WRITE_STATS, "max_seconds", 40.0)
+    assert st.update_ckpt(ck.max_write_seconds())
+    assert st.threshold == base + 30.0
+
+    class _Eng:
+        def busy(self):
+            return True
+
+    class _C:
+        pending = ck.Job(ckpt=None, path="x", keepalive=None, on_done=None, started=_t.perf_counter() - 15.0)
+        engine = _Eng()
+
+    monkeypatch.setattr(ck.Checkpointer, "_instances", {0: _C()})
+    rem = ck.inflight_remaining(st.max_ckpt)
+    assert 24.0 < rem <= 25.0
+    st.inflight_drain = rem
+    assert st.threshold > base + 30.0 + 24.0
