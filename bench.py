@@ -159,7 +159,7 @@ def main():
     fpt = num_flop_per_token(model.num_params(exclude_embedding=True), cfg)
     if rank == 0:
         out = {
-            "metric": "tokens/sec at seq=2048 bf16 (job aggregate over all GPUs; per-GPU in tokens_per_sec_per_gpu)",
+            "metric": f"tokens/sec at seq={S} bf16 (job aggregate over all GPUs; per-GPU in tokens_per_sec_per_gpu)",
             "value": round(tps, 2),
             "unit": "tokens/s",
             "n_gpus": world,

@@ -142,11 +142,27 @@ class Checkpointer:
         self.engine = _ext.native().CkptEngine(device_index)
         self.pending: Optional["Job"] = None
         self.staged = False
+        self._prewarm: Optional[threading.Thread] = None
+
+    def prewarm(self, nbytes: int):
+        """Allocate the pinned staging pool in the background (hipHostMalloc of tens of GB takes
+        seconds), so the first async checkpoint does not stall training on it."""
+        if self._prewarm is not None or nbytes <= self.engine.pool_size():
+            return
+        self._prewarm = threading.Thread(target=self.engine.reserve, args=(int(nbytes),), daemon=True,
+                                         name="pyrecover-ckpt-prewarm")
+        self._prewarm.start()
+
+    def _join_prewarm(self):
+        if self._prewarm is not None:
+            self._prewarm.join()
+            self._prewarm = None
 
     # -- staging -------------------------------------------------------------------------
     def stage(self, obj):
         """Snapshot every tensor of ``obj`` on this checkpointer's device into the pinned pool;
         return ``obj`` rebuilt with CPU tensors aliasing the pool (other tensors are cloned)."""
+        self._join_prewarm()
         self.wait()  # pool reuse: the previous archive must be on disk
         dev_is_cuda = self.device_index >= 0
         ts = _tensors(obj, [])

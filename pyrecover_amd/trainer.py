@@ -173,6 +173,10 @@ def train(args):
             log_rank0("--compile: no GPU, running eagerly")
     eager_steps_this_run = 0
     step_timer = _StepTimer(use_cuda)
+    if args.async_checkpoint and int(args.checkpoint_frequency) != -1 and use_cuda:
+        # params + AdamW moments (+ slack for the small entries); sharded saves need ~1/W of it
+        est = 3 * flat.numel * flat.data.element_size() // (world_size if args.use_torch_distributed_ckpt else 1)
+        ckcore.Checkpointer.get(device).prewarm(int(est * 1.05) + (64 << 20))
     num_flop_per_token_ = num_flop_per_token(model.num_params(exclude_embedding=True), model_config)
     log_rank0(f"Model parameters: {model.num_params() / 1e9:.3f} B, FLOPs/token: {num_flop_per_token_ / 1e9:.2f} G")
 
