@@ -388,8 +388,9 @@ void adamw_flat_(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, 
         "adamw_flat");
 }
 
-// dst = src^T for a 2-D 16-bit tensor (bf16/fp16) with R, C multiples of 64.
-at::Tensor transpose2d(const at::Tensor& src) {
+// dst = src^T for a 2-D 16-bit tensor (bf16/fp16) with R, C multiples of 64 (dst: optional
+// preallocated [C, R] row-major output).
+at::Tensor transpose2d(const at::Tensor& src, c10::optional<at::Tensor> out) {
   const Range range_("pyrecover::transpose2d");
   check_dev(src, "src");
   check_row_major(src, "src");
@@ -397,8 +398,19 @@ at::Tensor transpose2d(const at::Tensor& src) {
   const int64_t R = src.size(0), C = src.size(1);
   TORCH_CHECK(R % 64 == 0 && C % 64 == 0 && src.stride(0) % 8 == 0, "transpose2d: R, C must be multiples of 64");
   const c10::DeviceGuard guard(src.device());
-  at::Tensor dst = at::empty({C, R}, src.options());
-  check(pra_transpose16(src.data_ptr(), dst.data_ptr(), R, C, src.stride(0), R, stream_of(src)), "transpose2d");
+  at::Tensor dst;
+  if (out.has_value()) {
+    dst = *out;
+    same_dev(src, dst, "out");
+    check_row_major(dst, "out");
+    TORCH_CHECK(dst.size(0) == C && dst.size(1) == R && dst.scalar_type() == src.scalar_type() &&
+                    dst.stride(0) % 8 == 0,
+                "transpose2d: out must be [C, R] of the same dtype");
+  } else {
+    dst = at::empty({C, R}, src.options());
+  }
+  check(pra_transpose16(src.data_ptr(), dst.data_ptr(), R, C, src.stride(0), dst.stride(0), stream_of(src)),
+        "transpose2d");
   return dst;
 }
 
@@ -502,7 +514,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("bc1"), py::arg("bc2_sqrt"),
         py::arg("gscale"), py::arg("gscale_dev") = py::none(), py::arg("hyper_dev") = py::none());
   m.def("grad_norm", &grad_norm);
-  m.def("transpose2d", &transpose2d);
+  m.def("transpose2d", &transpose2d, py::arg("src"), py::arg("out") = py::none());
   m.def("swiglu_bwd_t_", &swiglu_bwd_t_);
   m.def("rope_t_", &rope_t_);
   m.def("attn_fwd", &attn_fwd);

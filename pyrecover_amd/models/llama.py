@@ -166,7 +166,23 @@ class Transformer(nn.Module):
         """Move all parameters/gradients into flat buffers (call after the final .to(device/dtype))."""
         if self.flat is None:
             self.flat = FlatParams(self.fusion_groups())
+            for mats in self._gemm_weights():
+                self.flat.register_transposed(mats, (sum(p.shape[0] for p in mats), mats[0].shape[1]))
+            # parameters written through the module API must refresh the transposed shadows
+            self.register_load_state_dict_post_hook(lambda mod, keys: mod.flat.refresh_transposed())
         return self.flat
+
+    def _gemm_weights(self) -> List[List[nn.Parameter]]:
+        out = []
+        for layer in self.layers.values():
+            at, ff = layer.attention, layer.feed_forward
+            out += [[at.wq.weight, at.wk.weight, at.wv.weight], [at.wo.weight], [ff.w1.weight, ff.w3.weight],
+                    [ff.w2.weight]]
+        out.append([self.output.weight])
+        return out
+
+    def _weight_t(self, params: Sequence[nn.Parameter]) -> Optional[torch.Tensor]:
+        return self.flat.weight_t(params) if self.flat is not None else None
 
     # ----------------------------------------------------------------------------------
     def _slot(self, params: Sequence[nn.Parameter]):
@@ -204,11 +220,13 @@ class Transformer(nn.Module):
                 x, n1 = self._norm(layer.attention_norm, h, pending)
             qkv_p = [at.wq.weight, at.wk.weight, at.wv.weight]
             att = F.attention_block(n1, self._weight(qkv_p), self._weight([at.wo.weight]), self._slot(qkv_p),
-                                    self._slot([at.wo.weight]), self.rope_tab, dims, qkv_p + [at.wo.weight])
+                                    self._slot([at.wo.weight]), self.rope_tab, dims, qkv_p + [at.wo.weight],
+                                    w_t=(self._weight_t(qkv_p), self._weight_t([at.wo.weight])))
             x2, n2 = self._norm(layer.ffn_norm, x, att)
             up = [ff.w1.weight, ff.w3.weight]
             mlp = F.swiglu_mlp(n2, self._weight(up), self._weight([ff.w2.weight]), self._slot(up),
-                               self._slot([ff.w2.weight]), up + [ff.w2.weight])
+                               self._slot([ff.w2.weight]), up + [ff.w2.weight],
+                               w_t=(self._weight_t(up), self._weight_t([ff.w2.weight])))
             h, pending = x2, mlp
         if pending is None:
             return self._norm(self.norm, h, None)
@@ -221,7 +239,8 @@ class Transformer(nn.Module):
         nf = self._trunk(tokens)
         W = self.output.weight
         if labels is not None:
-            return F.linear_cross_entropy(nf, self._weight([W]), labels, self._slot([W]), W, ignore_index)
+            return F.linear_cross_entropy(nf, self._weight([W]), labels, self._slot([W]), W, ignore_index,
+                                          w_t=self._weight_t([W]))
         return torch.nn.functional.linear(nf, W)
 
     # ----------------------------------------------------------------------------------

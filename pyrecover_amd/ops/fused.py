@@ -256,8 +256,9 @@ class _AttentionBlock(torch.autograd.Function):
     """y = Wo · attn(rope(Wq x), rope(Wk x), Wv x) with a fused QKV GEMM."""
 
     @staticmethod
-    def forward(ctx, x, w_qkv, w_o, slot_qkv, slot_o, tab, dims, *params):
+    def forward(ctx, x, w_qkv, w_o, slot_qkv, slot_o, tab, dims, w_t, *params):
         B, S, Hq, Hkv, D, causal = dims
+        ctx.w_t = w_t  # transposed weight shadows (or None): faster data-gradient GEMM layout
         T = B * S
         dim = x.shape[-1]
         x2 = x.reshape(T, dim)
@@ -291,7 +292,8 @@ class _AttentionBlock(torch.autograd.Function):
         o2 = o.view(T, nq)
         # every read of a weight is enqueued BEFORE its gradient slot is published: a published
         # slot may be updated by the optimizer (overlapped with backward) on another stream.
-        do = torch.mm(dy2, w_o).view(B, S, Hq, D)
+        w_qkv_t, w_o_t = ctx.w_t if ctx.w_t is not None else (None, None)
+        do = (torch.mm(dy2, w_o_t.t()) if w_o_t is not None else torch.mm(dy2, w_o)).view(B, S, Hq, D)
         slot_o.mm_(dy2.t(), o2, tuple(w_o.shape))
         dqkv = torch.empty_like(qkv)
         q = qkv[:, :nq].view(B, S, Hq, D)
@@ -305,21 +307,23 @@ class _AttentionBlock(torch.autograd.Function):
             # inverse RoPE in place + dqkv^T in one pass, for the K-contiguous weight-grad GEMM
             C = _ext.require_for(dqkv)
             dqkvT = C.rope_t_(dqkv, nq + nk, tab, D, S, True)
-            dx = torch.mm(dqkv, w_qkv)
+            dx = torch.mm(dqkv, w_qkv_t.t()) if w_qkv_t is not None else torch.mm(dqkv, w_qkv)
             slot_qkv.mm_(dqkvT, C.transpose2d(x2).t(), tuple(w_qkv.shape))
         else:
             if dqkv.is_cuda:
                 _ext.require_for(dqkv).rope_(dqkv, nq + nk, tab, D, S, 0, True)
             else:
                 ref.rope_inplace_2d(dqkv, nq + nk, tab, D, S, inverse=True)
-            dx = torch.mm(dqkv, w_qkv)
+            dx = torch.mm(dqkv, w_qkv_t.t()) if w_qkv_t is not None else torch.mm(dqkv, w_qkv)
             _wgrad_into(slot_qkv, dqkv, x2, tuple(w_qkv.shape))
-        n_params = ctx.needs_input_grad.__len__() - 7
-        return (dx.view(B, S, -1), None, None, None, None, None, None) + (None,) * n_params
+        n_params = ctx.needs_input_grad.__len__() - 8
+        return (dx.view(B, S, -1), None, None, None, None, None, None, None) + (None,) * n_params
 
 
-def attention_block(x, w_qkv, w_o, slot_qkv, slot_o, tab, dims, params):
-    return _AttentionBlock.apply(x, w_qkv, w_o, slot_qkv, slot_o, tab, dims, *params)
+def attention_block(x, w_qkv, w_o, slot_qkv, slot_o, tab, dims, params, w_t=None):
+    if w_t is not None and any(t is None for t in w_t):
+        w_t = None
+    return _AttentionBlock.apply(x, w_qkv, w_o, slot_qkv, slot_o, tab, dims, w_t, *params)
 
 
 # ---------------------------------------------------------------------------------------
@@ -345,7 +349,8 @@ class _SwiGLUMLP(torch.autograd.Function):
     """y = W2 (silu(W1 x) * (W3 x)) with W1|W3 fused into one GEMM."""
 
     @staticmethod
-    def forward(ctx, x, w13, w2, slot13, slot2, *params):
+    def forward(ctx, x, w13, w2, slot13, slot2, w_t, *params):
+        ctx.w_t = w_t
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
         gu = torch.mm(x2, w13.t())
@@ -361,24 +366,27 @@ class _SwiGLUMLP(torch.autograd.Function):
         slot13, slot2 = ctx.slots
         shape = dy.shape
         dy2 = dy.reshape(-1, shape[-1])
-        da = torch.mm(dy2, w2)
+        w13_t, w2_t = ctx.w_t if ctx.w_t is not None else (None, None)
+        da = torch.mm(dy2, w2_t.t()) if w2_t is not None else torch.mm(dy2, w2)
         slot2.mm_(dy2.t(), a, tuple(w2.shape))
         if TN_WGRAD and _tn_ok(gu) and _tn_ok(x2) and _tn_ok(da):
             # SwiGLU backward in place over gu, writing dgu^T in the same pass
             C = _ext.require_for(gu)
             dguT = C.swiglu_bwd_t_(da, gu)
-            dx = torch.mm(gu, w13)
+            dx = torch.mm(gu, w13_t.t()) if w13_t is not None else torch.mm(gu, w13)
             slot13.mm_(dguT, C.transpose2d(x2).t(), tuple(w13.shape))
         else:
             dgu = _swiglu_bwd_(da, gu)  # in place over gu (dead after this)
-            dx = torch.mm(dgu, w13)
+            dx = torch.mm(dgu, w13_t.t()) if w13_t is not None else torch.mm(dgu, w13)
             _wgrad_into(slot13, dgu, x2, tuple(w13.shape))
-        n_params = len(ctx.needs_input_grad) - 5
-        return (dx.view(shape), None, None, None, None) + (None,) * n_params
+        n_params = len(ctx.needs_input_grad) - 6
+        return (dx.view(shape), None, None, None, None, None) + (None,) * n_params
 
 
-def swiglu_mlp(x, w13, w2, slot13, slot2, params):
-    return _SwiGLUMLP.apply(x, w13, w2, slot13, slot2, *params)
+def swiglu_mlp(x, w13, w2, slot13, slot2, params, w_t=None):
+    if w_t is not None and any(t is None for t in w_t):
+        w_t = None
+    return _SwiGLUMLP.apply(x, w13, w2, slot13, slot2, w_t, *params)
 
 
 # ---------------------------------------------------------------------------------------
@@ -387,7 +395,8 @@ class _LinearCrossEntropy(torch.autograd.Function):
     dlogits in place during the backward."""
 
     @staticmethod
-    def forward(ctx, h, w_out, labels, slot, ignore_index, weight_param):
+    def forward(ctx, h, w_out, labels, slot, ignore_index, w_t, weight_param):
+        ctx.w_t = w_t
         h2 = h.reshape(-1, h.shape[-1])
         lab = labels.reshape(-1).contiguous()
         logits = torch.mm(h2, w_out.t())
@@ -419,13 +428,13 @@ class _LinearCrossEntropy(torch.autograd.Function):
             p[torch.arange(lab.numel()), lab.clamp_min(0)] -= valid.float()
             p = p * valid.float().unsqueeze(1) * (dloss.float() / n)
             dlogits = p.to(logits.dtype)
-        dh = torch.mm(dlogits, w_out)
+        dh = torch.mm(dlogits, ctx.w_t.t()) if ctx.w_t is not None else torch.mm(dlogits, w_out)
         _wgrad_into(ctx.slot, dlogits, h2, tuple(w_out.shape))
-        return dh.view(ctx.hshape), None, None, None, None, None
+        return dh.view(ctx.hshape), None, None, None, None, None, None
 
 
-def linear_cross_entropy(h, w_out, labels, slot, weight_param, ignore_index: int = -100):
-    return _LinearCrossEntropy.apply(h, w_out, labels, slot, ignore_index, weight_param)
+def linear_cross_entropy(h, w_out, labels, slot, weight_param, ignore_index: int = -100, w_t=None):
+    return _LinearCrossEntropy.apply(h, w_out, labels, slot, ignore_index, w_t, weight_param)
 
 
 # ---------------------------------------------------------------------------------------

@@ -95,6 +95,7 @@ class FlatAdamW(torch.optim.AdamW):
             _ext.require_for(f.data).adamw_flat_(f.data[lo:hi], f.grad[lo:hi], self.exp_avg[lo:hi],
                                                  self.exp_avg_sq[lo:hi], lr, b1, b2, eps, wd, bc1, bc2_sqrt,
                                                  self.grad_scale, self.grad_scale_dev, self.hyper)
+            f.refresh_transposed(lo, hi)  # same stream: the next backward sees the new weights
         else:
             self._step_reference(lr, b1, b2, eps, wd, bc1, bc2_sqrt, lo, hi)
 
@@ -165,6 +166,7 @@ class FlatAdamW(torch.optim.AdamW):
         if f.data.is_cuda:
             _ext.require_for(f.data).adamw_flat_(f.data, f.grad, self.exp_avg, self.exp_avg_sq, lr, b1, b2, eps, wd,
                                                  bc1, bc2_sqrt, self.grad_scale, self.grad_scale_dev, self.hyper)
+            f.refresh_transposed()
         else:
             self._step_reference(lr, b1, b2, eps, wd, bc1, bc2_sqrt)
         return loss

@@ -136,3 +136,4 @@ def broadcast_flat(flat: FlatParams, src: int = 0, group=None, chunk_mb: int = 1
     step = max(1, int(chunk_mb * 2 ** 20 / flat.data.element_size()))
     for o in range(0, n, step):
         dist.broadcast(flat.data[o:o + step], src=src, group=group)
+    flat.refresh_transposed()

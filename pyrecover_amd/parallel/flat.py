@@ -129,6 +129,58 @@ class FlatParams:
     def slot(self, p: torch.nn.Parameter) -> GradSlot:
         return self.slot_of[id(p)]
 
+    # --- transposed weight shadows (GPU) ---------------------------------------------------
+    # hipBLASLt runs the data-gradient GEMM dX = dY W about 10-15% faster with W supplied
+    # K-contiguous, i.e. in the forward GEMM's layout (tools/gemm_bench.py --layouts). Registered
+    # matrices keep a transposed copy in ``data_t`` (same offsets), refreshed by the optimizer right
+    # after it updates them (same stream, so never stale for the next backward) and by every path
+    # that loads parameters (checkpoint load, broadcast, load_state_dict).
+    def register_transposed(self, params: Sequence[torch.nn.Parameter], shape: Tuple[int, int]) -> bool:
+        rows, cols = shape
+        if not self.data.is_cuda or self.data.element_size() != 2 or rows % 64 or cols % 64:
+            return False
+        o = self.param_offset[id(params[0])]
+        if not hasattr(self, "t_mats"):
+            self.t_mats: List[Tuple[int, int, int]] = []
+            self.t_index: Dict[int, int] = {}
+            self.data_t = None
+        if o not in self.t_index:
+            self.t_index[o] = len(self.t_mats)
+            self.t_mats.append((o, rows, cols))
+            self.t_mats.sort()
+            self.t_index = {m[0]: i for i, m in enumerate(self.t_mats)}
+        return True
+
+    def weight_t(self, params: Sequence[torch.nn.Parameter]) -> Optional[torch.Tensor]:
+        """[cols, rows] transposed view of a registered fused weight, or None."""
+        if not getattr(self, "t_mats", None):
+            return None
+        o = self.param_offset[id(params[0])]
+        i = self.t_index.get(o)
+        if i is None:
+            return None
+        if self.data_t is None:
+            self.refresh_transposed()
+        _, rows, cols = self.t_mats[i]
+        return self.data_t[o:o + rows * cols].view(cols, rows)
+
+    def refresh_transposed(self, lo: int = 0, hi: Optional[int] = None):
+        """Re-derive the transposed copies of registered matrices inside [lo, hi), on the current
+        stream (call after anything that writes parameters)."""
+        if not getattr(self, "t_mats", None):
+            return
+        from .. import _ext
+
+        if self.data_t is None:
+            self.data_t = torch.empty_like(self.data)
+            lo, hi = 0, None
+        hi = self.numel if hi is None else hi
+        C = _ext.require_for(self.data)
+        for o, rows, cols in self.t_mats:
+            if lo <= o < hi:
+                C.transpose2d(self.data[o:o + rows * cols].view(rows, cols),
+                              self.data_t[o:o + rows * cols].view(cols, rows))
+
     # --- step protocol ----------------------------------------------------------------
     def rebind_grad(self, new: torch.Tensor):
         """Move the gradient space into ``new`` (same numel/dtype/device; e.g. an IPC-exportable

@@ -95,3 +95,43 @@ def test_training_is_deterministic(cuda):
     p0, _, _ = _train_steps(cuda, overlap=True, seed=5)
     p1, _, _ = _train_steps(cuda, overlap=True, seed=5)
     assert torch.equal(p0, p1)
+
+
+def test_transposed_weight_shadows_track_parameters(cuda):
+    """The transposed copies used by the data-gradient GEMMs equal W^T after optimizer steps
+    (overlapped and plain), load_state_dict, and in a fresh model."""
+    from pyrecover_amd.optim.adamw import FlatAdamW
+    from pyrecover_amd.parallel.ddp import GradReducer
+
+    torch.manual_seed(0)
+    a = get_preset("llama-tiny", seq_len=256)
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.bfloat16)
+    with torch.device(cuda):
+        m = Transformer(a)
+    torch.set_default_dtype(prev)
+    flat = m.flatten_()
+    mats = m._gemm_weights()
+
+    def check():
+        torch.cuda.synchronize()
+        for ps in mats:
+            wt = flat.weight_t(ps)
+            assert wt is not None
+            assert torch.equal(wt, flat.weight(ps, (sum(p.shape[0] for p in ps), ps[0].shape[1])).t())
+
+    check()
+    for overlap in (True, False):
+        red = GradReducer(flat, bucket_cap_mb=0.5, first_bucket_mb=0.25)
+        opt = FlatAdamW(flat, lr=1e-2)
+        if overlap:
+            opt.enable_overlap(red)
+        t = torch.randint(0, a.vocab_size, (2, 257), device=cuda)
+        opt.zero_grad()
+        m(t[:, :-1], labels=t[:, 1:]).backward()
+        red.finish()
+        opt.step()
+        check()
+    sd = {k: v.clone() * 0.5 for k, v in m.state_dict().items()}
+    m.load_state_dict(sd)
+    check()

@@ -39,9 +39,10 @@ def main():
         cases = {"fwd": lambda: torch.mm(x, w.t()), "dgrad": lambda: torch.mm(dy, w),
                  "wgrad": lambda: torch.mm(dy.t(), x)}
         if a.layouts:  # K-contiguous (transposed) activations: wgrad as a "TN" GEMM
-            dyT, xT = dy.t().contiguous(), x.t().contiguous()
+            dyT, xT, wT = dy.t().contiguous(), x.t().contiguous(), w.t().contiguous()
             cases.update({"wgrad_tn": lambda: torch.mm(dyT, xT.t()), "wgrad_dyT_x": lambda: torch.mm(dyT, x),
                           "dgrad_from_dyT": lambda: torch.mm(dyT.t(), w),
+                          "dgrad_wT": lambda: torch.mm(dy, wT.t()),
                           "transpose_dy": lambda: dy.t().contiguous(), "transpose_x": lambda: x.t().contiguous()})
         for cname, fn in cases.items():
             for _ in range(3):
