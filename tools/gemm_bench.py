@@ -43,6 +43,7 @@ def main():
             cases.update({"wgrad_tn": lambda: torch.mm(dyT, xT.t()), "wgrad_dyT_x": lambda: torch.mm(dyT, x),
                           "dgrad_from_dyT": lambda: torch.mm(dyT.t(), w),
                           "dgrad_wT": lambda: torch.mm(dy, wT.t()),
+                          "dgrad_TT": lambda: torch.mm(dyT.t(), wT.t()),
                           "transpose_dy": lambda: dy.t().contiguous(), "transpose_x": lambda: x.t().contiguous()})
         for cname, fn in cases.items():
             for _ in range(3):
