@@ -528,13 +528,13 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
 //   S^T = K Q^T, dP^T = V dO^T (query on lane; lse/delta are lane constants)
 //   dQ^T += K^T dS^T
 // ======================================================================================
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void bwd_dq_kernel(
+template <int D, bool CAUSAL, int NW>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
     const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ V,
     const __bf16* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
     __bf16* __restrict__ dQ, int S, int Hq, int Hkv, long ldq, long ldk, long ldv, long lddo, long lddq,
     float scale, float scale_log2) {
-  constexpr int KT = 64, QT = 128;
+  constexpr int KT = 64, QT = 32 * NW;
   constexpr int NKS = D / 16, NDB = D / 32, TILE = KT * D;
   __shared__ __attribute__((aligned(16))) __bf16 smem[4 * TILE];  // K0 V0 K1 V1
 
@@ -581,7 +581,7 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(
   const int kend = CAUSAL ? min(S, q0 + QT) : S;
   const int nkt = (kend + KT - 1) / KT;
 
-  GStage<D, KT> gk, gv;
+  GStage<D, KT, NW> gk, gv;
   gk.init(ldk);
   gv.init(ldv);
   gk.issue(Kb, smem);
@@ -719,13 +719,23 @@ hipError_t pra_attn_bwd(const void* q, const void* k, const void* v, const void*
 #undef LAUNCH
   }
   {
-    dim3 grid(((S + 127) / 128) * Hq * B);
-#define LAUNCH(DD, CC)                                                                                         \
-  hipLaunchKernelGGL((bwd_dq_kernel<DD, CC>), grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,       \
-                     (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dq, S, Hq, Hkv, ldq, ldk, ldv,   \
-                     lddo, lddq, scale, sl2)
-    if (D == 128) { if (causal) LAUNCH(128, true); else LAUNCH(128, false); }
-    else { if (causal) LAUNCH(64, true); else LAUNCH(64, false); }
+    static const int dq_env = [] {
+      const char* e = getenv("PRA_DQ_NW");
+      return e ? atoi(e) : 0;
+    }();
+    const int nwq = (dq_env == 4 || S % 256) ? 4 : 8;
+    dim3 grid(((S + 32 * nwq - 1) / (32 * nwq)) * Hq * B);
+#define LAUNCH(DD, CC, NWW)                                                                                     \
+  hipLaunchKernelGGL((bwd_dq_kernel<DD, CC, NWW>), grid, dim3(NWW * 64), 0, st, (const __bf16*)q,               \
+                     (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dq, S, Hq, Hkv,  \
+                     ldq, ldk, ldv, lddo, lddq, scale, sl2)
+    if (nwq == 8) {
+      if (D == 128) { if (causal) LAUNCH(128, true, 8); else LAUNCH(128, false, 8); }
+      else { if (causal) LAUNCH(64, true, 8); else LAUNCH(64, false, 8); }
+    } else {
+      if (D == 128) { if (causal) LAUNCH(128, true, 4); else LAUNCH(128, false, 4); }
+      else { if (causal) LAUNCH(64, true, 4); else LAUNCH(64, false, 4); }
+    }
 #undef LAUNCH
   }
   return hipGetLastError();
