@@ -87,7 +87,11 @@ def load_state_into(model, optimizer, lr_scheduler, sampler, ckpt) -> Tuple[int,
     if optimizer is not None and "optimizer" in ckpt:
         optimizer.load_state_dict(ckpt["optimizer"])
     if lr_scheduler is not None and "lr_scheduler" in ckpt:
-        lr_scheduler.load_state_dict(ckpt["lr_scheduler"])
+        sd = dict(ckpt["lr_scheduler"])
+        if hasattr(lr_scheduler, "lr_lambdas"):
+            # dcp drops the list of (empty) lambda states when flattening; LambdaLR needs it back
+            sd.setdefault("lr_lambdas", [None] * len(sd.get("base_lrs", lr_scheduler.lr_lambdas)))
+        lr_scheduler.load_state_dict(sd)
     if sampler is not None and "sampler_state" in ckpt and hasattr(sampler, "load_state_dict"):
         sampler.load_state_dict(ckpt["sampler_state"])
     ps = ckpt.get("pyrecover_state") or {}

@@ -166,6 +166,8 @@ class Transformer(nn.Module):
         """Move all parameters/gradients into flat buffers (call after the final .to(device/dtype))."""
         if self.flat is None:
             self.flat = FlatParams(self.fusion_groups())
+            # optimizer-state indices follow model.parameters() order, as in the reference
+            self.flat.module_order = list(self.parameters())
             for mats in self._gemm_weights():
                 self.flat.register_transposed(mats, (sum(p.shape[0] for p in mats), mats[0].shape[1]))
             # parameters written through the module API must refresh the transposed shadows

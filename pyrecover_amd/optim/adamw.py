@@ -21,7 +21,9 @@ from ..parallel.flat import FlatParams
 class FlatAdamW(torch.optim.AdamW):
     def __init__(self, flat: FlatParams, params=None, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 1e-2, fused: Optional[bool] = None, grad_scale: float = 1.0):
-        params = list(params) if params is not None else list(flat.params)
+        # default order = the model's parameters() order when the model recorded it (the
+        # reference's optimizer-state indices), else the flat buffer order
+        params = list(params) if params is not None else list(getattr(flat, "module_order", None) or flat.params)
         for p in params:
             if id(p) not in flat.param_offset:
                 raise ValueError("every optimized parameter must live in the flat buffer")

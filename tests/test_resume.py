@@ -148,3 +148,90 @@ def test_baseline_config1_gpt2_small_fp32_cpu(tmp_path):
     for (k, a), (_, b) in zip(m.state_dict().items(), m2.state_dict().items()):
         assert torch.equal(a, b), k
     assert torch.equal(o.exp_avg_sq, o2.exp_avg_sq) and s.state_dict() == s2.state_dict()
+
+
+def test_imports_reference_dcp_checkpoint(tmp_path):
+    """A checkpoint written the way the reference writes its sharded format (dcp.save of the
+    nn.Module, the torch.optim.AdamW and the LambdaLR objects, reference checkpoint.py:252-274)
+    loads into the flat model / FlatAdamW with identical weights and moments."""
+    import torch.distributed.checkpoint as dcp
+
+    from pyrecover_amd.ckpt.sharded import load_ckpt_distributed
+    from pyrecover_amd.config import get_preset
+    from pyrecover_amd.models.llama import Transformer
+    from pyrecover_amd.optim.adamw import FlatAdamW
+    from pyrecover_amd.optim.lr import build_lr_scheduler
+
+    torch.manual_seed(0)
+    a = get_preset("llama-micro", seq_len=64)
+    ref_model = Transformer(a)
+    ref_opt = torch.optim.AdamW(ref_model.parameters(), lr=1e-3)
+    ref_sched = build_lr_scheduler(ref_opt, 2)
+    tok = torch.randint(0, a.vocab_size, (2, 65))
+    ref_opt.zero_grad()
+    ref_model(tok[:, :-1], labels=tok[:, 1:]).backward()
+    ref_opt.step()
+    ref_sched.step()
+    path = tmp_path / "exp" / "ckpt_1"
+    path.parent.mkdir(parents=True)
+    dcp.save({"model": ref_model, "optimizer": ref_opt, "metadata": {"epoch": 1, "step": 1},
+              "lr_scheduler": ref_sched}, checkpoint_id=str(path), storage_writer=dcp.FileSystemWriter(str(path)))
+
+    torch.manual_seed(1)
+    m = Transformer(a)
+    flat = m.flatten_()
+    opt = FlatAdamW(flat, lr=1e-3)
+    sched = build_lr_scheduler(opt, 2)
+    epoch, step = load_ckpt_distributed(m, opt, sched, None, str(path))
+    assert (epoch, step) == (1, 1)
+    ref_sd = ref_model.state_dict()
+    for k, v in m.state_dict().items():
+        assert torch.equal(v, ref_sd[k]), k
+    ref_st = ref_opt.state_dict()["state"]
+    for i, p in enumerate(m.parameters()):
+        assert torch.equal(opt.state[p]["exp_avg"], ref_st[i]["exp_avg"])
+        assert torch.equal(opt.state[p]["exp_avg_sq"], ref_st[i]["exp_avg_sq"])
+    assert sched.last_epoch == ref_sched.last_epoch
+
+
+def test_imports_reference_vanilla_checkpoint(tmp_path):
+    """A `.pt` written the way the reference writes it (torch.save of model/optimizer/scheduler
+    state dicts, reference checkpoint.py:58-84) resumes into the flat model / FlatAdamW with the
+    same weights, moments and schedule; our own vanilla save of the same state has the same
+    optimizer index -> tensor mapping."""
+    from pyrecover_amd.ckpt.vanilla import load_ckpt_vanilla, save_ckpt_vanilla
+    from pyrecover_amd.config import get_preset
+    from pyrecover_amd.models.llama import Transformer
+    from pyrecover_amd.optim.adamw import FlatAdamW
+    from pyrecover_amd.optim.lr import build_lr_scheduler
+
+    torch.manual_seed(0)
+    a = get_preset("llama-micro", seq_len=64)
+    ref_model = Transformer(a)
+    ref_opt = torch.optim.AdamW(ref_model.parameters(), lr=1e-3)
+    ref_sched = build_lr_scheduler(ref_opt, 2)
+    tok = torch.randint(0, a.vocab_size, (2, 65))
+    ref_opt.zero_grad()
+    ref_model(tok[:, :-1], labels=tok[:, 1:]).backward()
+    ref_opt.step()
+    ref_sched.step()
+    p = tmp_path / "exp" / "ckpt_1.pt"
+    p.parent.mkdir(parents=True)
+    torch.save({"epoch": 1, "step": 1, "model": ref_model.state_dict(), "optimizer": ref_opt.state_dict(),
+                "lr_scheduler": ref_sched.state_dict()}, p)
+
+    m = Transformer(a)
+    flat = m.flatten_()
+    opt = FlatAdamW(flat, lr=1e-3)
+    sched = build_lr_scheduler(opt, 2)
+    assert load_ckpt_vanilla(m, opt, sched, None, str(p), verify=False) == (1, 1)
+    ref_st = ref_opt.state_dict()["state"]
+    for i, q in enumerate(m.parameters()):
+        assert torch.equal(q, dict(ref_model.named_parameters())[list(dict(m.named_parameters()))[i]])
+        assert torch.equal(opt.state[q]["exp_avg"], ref_st[i]["exp_avg"])
+    # round trip through our writer keeps the reference's index -> tensor mapping
+    p2 = tmp_path / "exp" / "ckpt_2.pt"
+    save_ckpt_vanilla(m, opt, sched, None, 2, 1, str(p2), max_keep=0, verify=False)
+    ours = torch.load(p2, weights_only=True)["optimizer"]["state"]
+    for i in ref_st:
+        assert torch.equal(ours[i]["exp_avg_sq"], ref_st[i]["exp_avg_sq"]), i
