@@ -241,6 +241,23 @@ at::Tensor swiglu_bwd(const at::Tensor& dy, const at::Tensor& gu, c10::optional<
   return dgu;
 }
 
+// gu: [T, 2F] -> (a [T, F], a^T [F, T]) in one pass (same math as swiglu_fwd).
+std::vector<at::Tensor> swiglu_fwd_t(const at::Tensor& gu) {
+  const Range range_("pyrecover::swiglu_fwd_t");
+  check_dev(gu, "gu");
+  check_row_major(gu, "gu");
+  const int64_t T = gu.size(0), F = gu.size(1) / 2;
+  TORCH_CHECK(gu.element_size() == 2, "swiglu_fwd_t: 16-bit dtype required");
+  TORCH_CHECK(T % 64 == 0 && F % 64 == 0 && gu.size(1) == 2 * F, "swiglu_fwd_t: tokens and F must be multiples of 64");
+  const c10::DeviceGuard guard(gu.device());
+  at::Tensor a = at::empty({T, F}, gu.options());
+  at::Tensor aT = at::empty({F, T}, gu.options());
+  check(pra_swiglu_fwd_t(dt(gu), gu.data_ptr(), a.data_ptr(), aT.data_ptr(), T, (int)F, (int)gu.stride(0), (int)F,
+                         stream_of(gu)),
+        "swiglu_fwd_t");
+  return {a, aT};
+}
+
 // In place: gu <- [dg | du] (the SwiGLU backward, same math as swiglu_bwd); returns dgu^T [2F, T].
 at::Tensor swiglu_bwd_t_(const at::Tensor& dy, at::Tensor gu) {
   const Range range_("pyrecover::swiglu_bwd_t");
@@ -516,6 +533,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("grad_norm", &grad_norm);
   m.def("transpose2d", &transpose2d, py::arg("src"), py::arg("out") = py::none());
   m.def("swiglu_bwd_t_", &swiglu_bwd_t_);
+  m.def("swiglu_fwd_t", &swiglu_fwd_t);
   m.def("rope_t_", &rope_t_);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);

@@ -324,33 +324,56 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_kernel(const __bf16* __restric
 
 // ======================================================================================
 // Backward preprocess: delta[b,h,q] = sum_d dO[q,h,d] * O[q,h,d]  (fp32)
+// Block = (b, PRE_QB consecutive queries, all heads): the [PRE_QB, Hq, D] slabs of O and dO are
+// contiguous per token, so the reads stream at full width with 4 rows in flight per lane; the
+// per-row sums are staged in LDS and written out along q (runs of PRE_QB floats per head) instead
+// of one scattered 4-B store per row.
 // ======================================================================================
+constexpr int PRE_QB = 16;
+constexpr int PRE_MAXH = 128;
 template <int D>
 __global__ __launch_bounds__(256) void bwd_pre_kernel(const __bf16* __restrict__ O, const __bf16* __restrict__ dO,
                                                       float* __restrict__ delta, int B, int S, int Hq, long ldo,
                                                       long lddo) {
-  constexpr int LPR = D / 8;            // lanes per row
-  constexpr int RPB = 256 / LPR;        // rows per block
-  const long row = (long)blockIdx.x * RPB + threadIdx.x / LPR;  // row = (b*S + q)*Hq + h
+  constexpr int LPR = D / 8;     // lanes per row
+  constexpr int RPP = 256 / LPR;  // rows per pass
+  constexpr int U = 4;           // passes in flight
+  __shared__ float red[PRE_QB * (PRE_MAXH + 1)];
+  const int nqb = S / PRE_QB;
+  const int b = blockIdx.x / nqb, q0 = (blockIdx.x % nqb) * PRE_QB;
+  const int rows = PRE_QB * Hq;  // row r = qi * Hq + h
   const int sub = threadIdx.x % LPR;
-  const long total = (long)B * S * Hq;
-  float acc = 0.f;
-  if (row < total) {
-    const long bq = row / Hq;
-    const int h = (int)(row % Hq);
-    float a[8], c[8];
-    load8<__bf16>(O + bq * ldo + h * D + sub * 8, a);
-    load8<__bf16>(dO + bq * lddo + h * D + sub * 8, c);
+  const long tok0 = (long)b * S + q0;
+  for (int base = threadIdx.x / LPR; base < rows; base += RPP * U) {
+    float a[U][8], c[U][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc += a[j] * c[j];
+    for (int u = 0; u < U; ++u) {
+      const int r = base + u * RPP;
+      if (r < rows) {
+        const long t = tok0 + r / Hq;
+        const int h = r % Hq;
+        load8<__bf16>(O + t * ldo + h * D + sub * 8, a[u]);
+        load8<__bf16>(dO + t * lddo + h * D + sub * 8, c[u]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[u][j] = c[u][j] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += a[u][j] * c[u][j];
+#pragma unroll
+      for (int off = LPR / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+      const int r = base + u * RPP;
+      if (r < rows && sub == 0) red[(r / Hq) * (PRE_MAXH + 1) + r % Hq] = acc;
+    }
   }
-#pragma unroll
-  for (int off = LPR / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-  if (row < total && sub == 0) {
-    const long bq = row / Hq;
-    const int h = (int)(row % Hq);
-    const long b = bq / S, q = bq % S;
-    delta[(b * Hq + h) * S + q] = acc;
+  __syncthreads();
+  for (int i = threadIdx.x; i < rows; i += 256) {
+    const int h = i / PRE_QB, qi = i % PRE_QB;
+    delta[((long)b * Hq + h) * S + q0 + qi] = red[qi * (PRE_MAXH + 1) + h];
   }
 }
 
@@ -688,9 +711,8 @@ hipError_t pra_attn_bwd(const void* q, const void* k, const void* v, const void*
     return hipErrorInvalidValue;
   const float sl2 = scale * 1.4426950408889634f;
   {
-    const int rpb = 256 / (D / 8);
-    const long rows = (long)B * S * Hq;
-    const int grid = (int)((rows + rpb - 1) / rpb);
+    if (Hq > PRE_MAXH) return hipErrorInvalidValue;
+    const int grid = B * (S / PRE_QB);
     if (D == 128)
       hipLaunchKernelGGL((bwd_pre_kernel<128>), dim3(grid), dim3(256), 0, st, (const __bf16*)o,
                          (const __bf16*)dout, delta, B, S, Hq, ldo, lddo);

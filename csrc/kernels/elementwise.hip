@@ -202,6 +202,31 @@ __device__ __forceinline__ void put8(uint16_t* row, const float* v) {
   *reinterpret_cast<uint4*>(row) = *reinterpret_cast<const uint4*>(tmp);
 }
 
+// swiglu_fwd_t: a = silu(g) * u (row-major, for the W2 forward GEMM) and aT = a^T (K-contiguous
+// operand of the W2 weight-gradient GEMM, kept for the backward instead of a).
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_fwd_t_kernel(const T* __restrict__ gu, T* __restrict__ a,
+                                                           T* __restrict__ aT, int F, int ldgu, int lda, long ntok) {
+  __shared__ __attribute__((aligned(16))) uint16_t ta[64][72];
+  const long t0 = (long)blockIdx.y * 64;
+  const int c0 = blockIdx.x * 64;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = threadIdx.x + 256 * i, r = idx >> 3, ch = idx & 7;
+    const long t = t0 + r;
+    const int col = c0 + ch * 8;
+    float gv[8], uv[8], o[8];
+    load8<T>(gu + t * ldgu + col, gv);
+    load8<T>(gu + t * ldgu + F + col, uv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = rnd<T>(silu_f(gv[j])) * uv[j];  // identical to swiglu_fwd_kernel
+    store8<T>(a + t * lda + col, o);
+    put8<T>(&ta[r][ch * 8], o);
+  }
+  __syncthreads();
+  store_tile_t(ta, reinterpret_cast<uint16_t*>(aT), ntok, c0, t0);
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(const T* __restrict__ dy, T* gu, T* __restrict__ guT,
                                                            int F, int ldgu, int lddy, long ntok) {
@@ -332,6 +357,17 @@ hipError_t pra_transpose16(const void* src, void* dst, long R, long C, long ld_s
   dim3 grid((unsigned)(C / 64), (unsigned)(R / 64));
   hipLaunchKernelGGL((pra::transpose_kernel<uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)src, (uint16_t*)dst,
                      ld_src, ld_dst);
+  return hipGetLastError();
+}
+
+// a = swiglu(gu) [ntok, F] (ld lda) and aT = a^T [F, ntok]; ntok, F multiples of 64.
+hipError_t pra_swiglu_fwd_t(int dtype, const void* gu, void* a, void* aT, long ntok, int F, int ldgu, int lda,
+                            hipStream_t s) {
+  if (ntok % 64 || F % 64 || ldgu % 8 || lda % 8) return hipErrorInvalidValue;
+  dim3 grid((unsigned)(F / 64), (unsigned)(ntok / 64));
+  PRA_DISPATCH_16BIT(dtype, T,
+                     hipLaunchKernelGGL((pra::swiglu_fwd_t_kernel<T>), grid, dim3(256), 0, s, (const T*)gu, (T*)a,
+                                        (T*)aT, F, ldgu, lda, ntok));
   return hipGetLastError();
 }
 

@@ -29,6 +29,8 @@ hipError_t pra_embedding_fwd(int dtype, const int64_t* ids, const void* W, void*
 hipError_t pra_embedding_bwd(int dtype, const int64_t* sorted_ids, const int64_t* perm, const void* dout, void* dW,
                              long ntok, int D, long V, int accumulate, hipStream_t s);
 
+hipError_t pra_swiglu_fwd_t(int dtype, const void* gu, void* a, void* aT, long ntok, int F, int ldgu, int lda,
+                            hipStream_t s);
 hipError_t pra_swiglu_bwd_t(int dtype, const void* dy, void* gu, void* guT, long ntok, int F, int ldgu, int lddy,
                             hipStream_t s);
 hipError_t pra_rope_t(int dtype, void* x, void* xT, const void* tab, long ntok, int ld, int ncols, int nrot, int D,

@@ -79,7 +79,7 @@ def _mm_into(slot, a, b, shape):
 # Weight gradients dW = dY^T X with K = tokens. hipBLASLt runs this GEMM ~25-30% faster when both
 # operands are K-contiguous ("TN": dYt [out, T] times Xt [in, T]^T) than on the row-major
 # activations, which is worth two bandwidth-bound HIP transposes for the large projections
-# (QKV, W1|W3, output head; tools/gemm_bench.py --layouts). PYRECOVER_TN_WGRAD=0 disables it.
+# (QKV, W1|W3, W2, output head; tools/gemm_bench.py --layouts). PYRECOVER_TN_WGRAD=0 disables it.
 TN_WGRAD = os.environ.get("PYRECOVER_TN_WGRAD", "1") == "1"
 
 
@@ -354,9 +354,16 @@ class _SwiGLUMLP(torch.autograd.Function):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
         gu = torch.mm(x2, w13.t())
-        a = _swiglu_fwd(gu)
+        if TN_WGRAD and _tn_ok(gu) and (gu.shape[1] // 2) % 64 == 0:
+            # a^T (K-contiguous operand of the W2 weight gradient) is written in the same pass and
+            # kept instead of a
+            a, a_saved = _ext.require_for(gu).swiglu_fwd_t(gu)
+            ctx.a_is_t = True
+        else:
+            a = a_saved = _swiglu_fwd(gu)
+            ctx.a_is_t = False
         y = torch.mm(a, w2.t())
-        ctx.save_for_backward(x2, gu, a, w13, w2)
+        ctx.save_for_backward(x2, gu, a_saved, w13, w2)
         ctx.slots = (slot13, slot2)
         return y.view(shape)
 
@@ -368,7 +375,11 @@ class _SwiGLUMLP(torch.autograd.Function):
         dy2 = dy.reshape(-1, shape[-1])
         w13_t, w2_t = ctx.w_t if ctx.w_t is not None else (None, None)
         da = torch.mm(dy2, w2_t.t()) if w2_t is not None else torch.mm(dy2, w2)
-        slot2.mm_(dy2.t(), a, tuple(w2.shape))
+        if ctx.a_is_t:  # TN weight gradient: dW2 = (dY^T) (a^T)^T, both operands K-contiguous
+            dyT = _ext.require_for(dy2).transpose2d(dy2) if _tn_ok(dy2) else dy2.t()
+            slot2.mm_(dyT, a.t(), tuple(w2.shape))
+        else:
+            slot2.mm_(dy2.t(), a, tuple(w2.shape))
         if TN_WGRAD and _tn_ok(gu) and _tn_ok(x2) and _tn_ok(da):
             # SwiGLU backward in place over gu, writing dgu^T in the same pass
             C = _ext.require_for(gu)

@@ -268,6 +268,35 @@ def test_swiglu_bwd_t_matches_swiglu_bwd_exactly(cuda):
     assert torch.equal(guT, ref.t().contiguous())
 
 
+def test_swiglu_fwd_t_matches_swiglu_fwd_exactly(cuda):
+    C_ = _ext.native()
+    T, F = 256, 192
+    gu = torch.randn(T, 2 * F, device=cuda).bfloat16()
+    ref = C_.swiglu_fwd(gu)
+    a, aT = C_.swiglu_fwd_t(gu)
+    assert torch.equal(a, ref)
+    assert torch.equal(aT, ref.t().contiguous())
+
+
+def test_attention_bwd_delta_many_heads(cuda):
+    """Backward preprocess (delta = rowsum(dO * O), staged per query block in LDS) with a head count
+    that is not a power of two and D = 64: dq/dk/dv against the fp32 oracle."""
+    C = _ext.native()
+    B, S, Hq, Hkv, D = 1, 128, 12, 12, 64
+    q, k, v = (torch.randn(B, S, H, D, device=cuda).bfloat16() for H in (Hq, Hkv, Hkv))
+    scale = 1 / math.sqrt(D)
+    o, lse = C.attn_fwd(q, k, v, scale, True)
+    do = torch.randn_like(o)
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    C.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, True)
+    qf, kf, vf = (t.float().requires_grad_() for t in (q, k, v))
+    of = R.attention_ref(qf, kf, vf, causal=True, scale=scale)
+    of.backward(do.float())
+    assert _rel(dq, qf.grad) < 2e-2
+    assert _rel(dk, kf.grad) < 2e-2
+    assert _rel(dv, vf.grad) < 2e-2
+
+
 def test_rope_t_matches_rope_exactly(cuda):
     from pyrecover_amd.ops.reference import precompute_freqs_cis, rope_table
 

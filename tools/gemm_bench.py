@@ -22,16 +22,29 @@ def main():
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--no-table", action="store_true")
     ap.add_argument("--layouts", action="store_true", help="also time K-contiguous wgrad / transpose variants")
+    ap.add_argument("--only", default="", help="comma-separated subset of qkv,wo,w13,w2,head")
+    ap.add_argument("--tune", default="", help="tune missing shapes with TunableOp into this table "
+                                               "(seeded with the committed table)")
     a = ap.parse_args()
-    from pyrecover_amd.utils.gemm_tuning import configure_gemm_tuning
+    from pyrecover_amd.utils.gemm_tuning import TABLE, configure_gemm_tuning
 
-    configure_gemm_tuning("off" if a.no_table else "auto")
+    if a.tune:
+        import shutil
+
+        if not os.path.exists(a.tune):
+            shutil.copy(TABLE, a.tune)
+        configure_gemm_tuning("tune", table=a.tune)
+        torch.cuda.tunable.read_file(a.tune)
+    else:
+        configure_gemm_tuning("off" if a.no_table else "auto")
     dev = torch.device("cuda", 0)
     T, Dm, F, V = a.tokens, a.dim, a.ffn, a.vocab
     outs = {"qkv": 3 * Dm, "wo": Dm, "w13": 2 * F, "w2": Dm, "head": V}
     ins = {"qkv": Dm, "wo": Dm, "w13": Dm, "w2": F, "head": Dm}
     res = {}
     for name in outs:
+        if a.only and name not in a.only.split(","):
+            continue
         n_out, n_in = outs[name], ins[name]
         x = torch.randn(T, n_in, device=dev).bfloat16()
         w = torch.randn(n_out, n_in, device=dev).bfloat16()
@@ -61,6 +74,8 @@ def main():
     base = [k for k in res if k.split("_", 1)[1] in ("fwd", "dgrad", "wgrad")]
     tot_ms = sum(res[k]["ms"] for k in base if not k.startswith("head")) * 32 + sum(
         res[k]["ms"] for k in base if k.startswith("head"))
+    if a.tune:
+        torch.cuda.tunable.write_file()
     print(json.dumps({"table": not a.no_table, "gemm_ms_per_step": round(tot_ms, 1), "shapes": res}), flush=True)
 
 
