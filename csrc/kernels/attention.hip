@@ -21,8 +21,13 @@
 //    head) and dQ (queries resident, K/V tiles by LDS-DMA, loop over key tiles). P is
 //    recomputed from the saved log-sum-exp. Both run at 2 waves per SIMD with no spills.
 //
+//  * long query loops (S * Hq/Hkv >= 8192) use a dK/dV kernel with one wave per SIMD and two query
+//    sub-tiles in flight (bwd_dkdv_p2_kernel); the dQ kernel interleaves the softmax of one 32-key
+//    half between the MFMAs of the other (PIPE). Both schedules are explicit sched_barrier regions.
+//
 // Measured on MI355X (tools/attn_bench.py, B4 S2048 H32 D128 causal): fwd 0.214 ms (640 TF),
 // bwd 0.645 ms (530 TF at the 2.5x-forward convention); B16 H64/8 non-causal fwd 835 TF.
+// B1 S8192 H32/8 causal: bwd 2.68 -> 1.91 ms with the pipelined kernels (719 TF model, 1.0 PF executed).
 #include "common.h"
 
 #include <stdlib.h>
@@ -395,7 +400,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
     const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ V,
     const __bf16* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
     __bf16* __restrict__ dK, __bf16* __restrict__ dV, int S, int Hq, int Hkv, long ldq, long ldk, long ldv,
-    long lddo, long lddk, long lddv, float scale, float scale_log2) {
+    long lddo, long lddk, long lddv, float scale, float scale_log2, int prio) {
   constexpr int KB = 32 * NW, QT = 32, NT = NW * 64;
   constexpr int NKS = D / 16, NDB = D / 32;
   constexpr int KVT = KB * D, QDT = QT * D;
@@ -453,6 +458,9 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
     if (ROWC_LDS && wid == 0) rc_next = rc_base[(long)hq * S + q0] * rc_mul;
   };
   if (total > 0) stage_load(0);
+  // one wave per SIMD runs ahead: its MFMA chains win issue, so its softmax VALU overlaps the
+  // partner wave's MFMAs instead of both waves alternating MFMA and VALU phases in lockstep
+  if (prio && NW == 8 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
 
   for (int it = 0; it < total; ++it) {
     const int hq = hk * nrep + it / nqt;
@@ -546,17 +554,202 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
 }
 
 // ======================================================================================
+// Backward dK/dV, one wave per SIMD, two query sub-tiles in flight: block = (b, kv head, 128
+// keys), 4 waves x 32 keys; each step stages 64 queries (sub-tiles A and B of 32). With the whole
+// 512-entry register file per wave, a wave keeps S/dP of both sub-tiles live and runs them as a
+// two-stage pipeline, the softmax VALU of one sub-tile interleaved (sched_group_barrier) between
+// the MFMAs of the other -- instead of two waves per SIMD alternating MFMA and VALU phases in
+// lockstep between barriers (bwd_dkdv_kernel):
+//   [S,dP of A] -> [S,dP of B | softmax A] -> [dV,dK += A | softmax B] -> [dV,dK += B]
+// K/V of the block stay in LDS (64 KB at D = 128). Q/dO steps (32 KB) and their per-query
+// constants (lse*log2e, delta) arrive by LDS-DMA into a double buffer, issued one step ahead.
+// ======================================================================================
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 1) void bwd_dkdv_p2_kernel(
+    const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ V,
+    const __bf16* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
+    __bf16* __restrict__ dK, __bf16* __restrict__ dV, int S, int Hq, int Hkv, long ldq, long ldk, long ldv,
+    long lddo, long lddk, long lddv, float scale, float scale_log2) {
+  constexpr int NW = 4, KB = 32 * NW, QS = 64;
+  constexpr int NKS = D / 16, NDB = D / 32;
+  constexpr int KVT = KB * D, QDT = QS * D;
+  // Q0 dO0 Q1 dO1 (steps, double-buffered) | K V | row constants [buf][lse, delta][64]
+  __shared__ __attribute__((aligned(16))) __bf16 smem[4 * QDT + 2 * KVT];
+  __shared__ __attribute__((aligned(16))) float rowc[2][2][QS];
+  __bf16* const Ks = smem + 4 * QDT;
+  __bf16* const Vs = Ks + KVT;
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h2 = lane >> 5, l32 = lane & 31;
+  const int nkb = S / KB;
+  const int BH = gridDim.x / nkb;
+  const int kbk = (int)(blockIdx.x / BH);  // causal: early key blocks have the most work
+  const int bh = blockIdx.x % BH;
+  const int hk = bh % Hkv, b = bh / Hkv;
+  const int nrep = Hq / Hkv;
+  const int k0 = kbk * KB, kw = k0 + wid * 32;
+
+  GStage<D, QS, NW> gq, gd;
+  gq.init(ldq);
+  gd.init(lddo);
+  const int qstart = CAUSAL ? k0 : 0;
+  const int nqs = (S - qstart) / QS;
+  const int total = nqs * nrep;
+  auto issue_step = [&](int t, int buf) {
+    const int hq = hk * nrep + t / nqs;
+    const int q0 = qstart + (t % nqs) * QS;
+    gq.issue(Q + ((long)b * S + q0) * ldq + hq * D, smem + buf * 2 * QDT);
+    gd.issue(dO + ((long)b * S + q0) * lddo + hq * D, smem + buf * 2 * QDT + QDT);
+    if (wid < 2) {  // wave 0: lse, wave 1: delta (one dword per lane)
+      const float* src = (wid ? Delta : LSE) + ((long)b * Hq + hq) * S + q0 + lane;
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)&rowc[buf][wid][0], 4, 0, 0);
+    }
+  };
+  {
+    GStage<D, KB, NW> gk, gv;
+    gk.init(ldk);
+    gv.init(ldv);
+    gk.issue(K + ((long)b * S + k0) * ldk + hk * D, Ks);
+    gv.issue(V + ((long)b * S + k0) * ldv + hk * D, Vs);
+  }
+  if (total > 0) issue_step(0, 0);
+  const __bf16* Kw = Ks + wid * 32 * D;
+  const __bf16* Vw = Vs + wid * 32 * D;
+  LaneOff<D> lo;
+  lo.init(lane);
+
+  f32x16 dkt[NDB], dvt[NDB];
+#pragma unroll
+  for (int i = 0; i < NDB; ++i) { dkt[i] = f32x16{}; dvt[i] = f32x16{}; }
+  __syncthreads();  // K/V and step 0 have landed
+
+  for (int it = 0; it < total; ++it) {
+    const int cur = it & 1;
+    const int q0 = qstart + (it % nqs) * QS;
+    if (it + 1 < total) issue_step(it + 1, 1 - cur);  // lands under this step's MFMAs
+    const __bf16* Qs = smem + cur * 2 * QDT;
+    const __bf16* Ds = Qs + QDT;
+    const float* lrow = &rowc[cur][0][0];
+    const float* drow = &rowc[cur][1][0];
+
+    // a score (query q0 + 32 u + crow(r, h2), key kw + l32) is masked iff crow(r, 0) < lim - 32 u
+    //
+    // The step is written as 2 * (NKS + 2 NDB) explicit regions separated by sched_barrier(0), each
+    // issuing the LDS reads of the NEXT region's MFMA operands, its own two MFMAs, and a slice of the
+    // pending softmax (VALU), so every MFMA gap carries VALU work:
+    //   regions [0, NKS)            S, dP of sub-tile A
+    //   [NKS, 2 NKS)                S, dP of B        | softmax of A (16 / NKS rows per region)
+    //   [2 NKS, 2 NKS + 2 NDB)      dV, dK += A       | softmax of B
+    //   [2 NKS + 2 NDB, end)        dV, dK += B
+    auto step = [&](auto mask_c) {
+      constexpr bool MASK = decltype(mask_c)::value;
+      constexpr int R1 = NKS, R3 = 2 * NDB, NR = 2 * R1 + 2 * R3;
+      constexpr int EA = 16 / R1, EB = 16 / R3;  // softmax rows per region
+      const int lim = kw + l32 - q0 - 4 * h2;
+      f32x16 sa = f32x16{}, sb = f32x16{}, pa = f32x16{}, pb = f32x16{};
+      bf16x8 pA[2], gA[2], pB[2], gB[2];
+      f32x4 lc[4], dc[4];  // row constants of the sub-tile being softmaxed
+      auto fetch = [&](int k, bf16x8 (&o)[4]) {
+        if (k < 2 * R1) {
+          const int ks = k % R1, r0 = 32 * (k / R1);
+          o[0] = lo.rowk(Qs, r0, ks);
+          o[1] = lo.rowk(Kw, 0, ks);
+          o[2] = lo.rowk(Ds, r0, ks);
+          o[3] = lo.rowk(Vw, 0, ks);
+        } else if (k < NR) {
+          const int st = (k - 2 * R1) % R3, s2 = st / NDB, db = st % NDB, r0 = 32 * ((k - 2 * R1) / R3);
+          o[0] = lo.tr(Ds, r0 + 16 * s2, db);
+          o[1] = lo.tr(Qs, r0 + 16 * s2, db);
+        }
+      };
+      auto load_rc = [&](int u) {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          lc[rr] = *reinterpret_cast<const f32x4*>(lrow + 32 * u + 8 * rr + 4 * h2);
+          dc[rr] = *reinterpret_cast<const f32x4*>(drow + 32 * u + 8 * rr + 4 * h2);
+        }
+      };
+      auto soft = [&](f32x16& sv, f32x16& dp, int u, int r) {
+        float p = fexp2(fmaf(sv[r], scale_log2, -lc[r >> 2][r & 3] * 1.4426950408889634f));
+        if (MASK && crow(r, 0) < lim - 32 * u) p = 0.f;
+        sv[r] = p;
+        dp[r] = p * (dp[r] - dc[r >> 2][r & 3]);
+      };
+      bf16x8 cur[4], nxt[4];
+      fetch(0, cur);
+      load_rc(0);
+#pragma unroll
+      for (int k = 0; k < NR; ++k) {
+        fetch(k + 1, nxt);
+        if (k < R1) {
+          sa = mfma(cur[0], cur[1], sa);
+          pa = mfma(cur[2], cur[3], pa);
+        } else if (k < 2 * R1) {
+          sb = mfma(cur[0], cur[1], sb);
+          pb = mfma(cur[2], cur[3], pb);
+#pragma unroll
+          for (int e = 0; e < EA; ++e) soft(sa, pa, 0, (k - R1) * EA + e);
+          if (k == 2 * R1 - 1) {
+            pA[0] = pack8(sa, 0); pA[1] = pack8(sa, 1); gA[0] = pack8(pa, 0); gA[1] = pack8(pa, 1);
+            load_rc(1);
+          }
+        } else {
+          const int j = k - 2 * R1, st = j % R3, s2 = st / NDB, db = st % NDB;
+          const bool second = j >= R3;
+          dvt[db] = mfma(cur[0], second ? pB[s2] : pA[s2], dvt[db]);
+          dkt[db] = mfma(cur[1], second ? gB[s2] : gA[s2], dkt[db]);
+          if (!second) {
+#pragma unroll
+            for (int e = 0; e < EB; ++e) soft(sb, pb, 1, j * EB + e);
+            if (j == R3 - 1) {
+              pB[0] = pack8(sb, 0); pB[1] = pack8(sb, 1); gB[0] = pack8(pb, 0); gB[1] = pack8(pb, 1);
+            }
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) cur[i] = nxt[i];
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    // one code path (the causal mask is a per-element select that is a no-op off the diagonal
+    // band): a second instantiation makes the compiler shuffle the AGPR accumulators between them
+    if (!CAUSAL || q0 + QS - 1 >= kw) step(std::integral_constant<bool, CAUSAL>{});  // else fully masked
+    __syncthreads();  // next step landed (vmcnt(0) before the barrier); this step's buffer is free
+  }
+
+  const int krow = kw + l32;
+  __bf16* dkp = dK + ((long)b * S + krow) * lddk + hk * D;
+  __bf16* dvp = dV + ((long)b * S + krow) * lddv + hk * D;
+#pragma unroll
+  for (int db = 0; db < NDB; ++db)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      bf16x4 wk, wv;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        wk[jj] = (__bf16)(dkt[db][4 * rr + jj] * scale);
+        wv[jj] = (__bf16)(dvt[db][4 * rr + jj]);
+      }
+      *reinterpret_cast<bf16x4*>(dkp + db * 32 + 8 * rr + 4 * h2) = wk;
+      *reinterpret_cast<bf16x4*>(dvp + db * 32 + 8 * rr + 4 * h2) = wv;
+    }
+}
+
+// ======================================================================================
 // Backward dQ: block = (b, q head, 128 query rows), wave owns 32 queries; loop over 64-key tiles
 // (double-buffered in LDS, staged issue-early / write-late).
 //   S^T = K Q^T, dP^T = V dO^T (query on lane; lse/delta are lane constants)
 //   dQ^T += K^T dS^T
 // ======================================================================================
-template <int D, bool CAUSAL, int NW>
+// PIPE: the same tile work as explicit sched_barrier regions -- S/dP of the second 32-key half
+// interleaved with the softmax of the first, dQ of the first with the softmax of the second (see
+// bwd_dkdv_p2_kernel) -- instead of two back-to-back MFMA -> VALU -> MFMA halves.
+template <int D, bool CAUSAL, int NW, bool PIPE = false>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
     const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ V,
     const __bf16* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
     __bf16* __restrict__ dQ, int S, int Hq, int Hkv, long ldq, long ldk, long ldv, long lddo, long lddq,
-    float scale, float scale_log2) {
+    float scale, float scale_log2, int prio) {
   constexpr int KT = 64, QT = 32 * NW;
   constexpr int NKS = D / 16, NDB = D / 32, TILE = KT * D;
   __shared__ __attribute__((aligned(16))) __bf16 smem[4 * TILE];  // K0 V0 K1 V1
@@ -610,6 +803,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
   gk.issue(Kb, smem);
   gv.issue(Vb, smem + TILE);
   __syncthreads();
+  if (prio && NW == 8 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
 
   auto body = [&](auto cc, int kt) {
     constexpr int CUR = decltype(cc)::value;
@@ -620,6 +814,69 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
       gk.issue(Kb + (long)(k0 + KT) * ldk, smem + 2 * (1 - CUR) * TILE);
       gv.issue(Vb + (long)(k0 + KT) * ldv, smem + 2 * (1 - CUR) * TILE + TILE);
     }
+    if constexpr (PIPE) {
+      // a score (key k0 + 32 kb + crow(r, h2), query qrow) is masked iff crow(r, 0) > lim - 32 kb
+      auto tile = [&](auto mask_c) {
+        constexpr bool MASK = decltype(mask_c)::value;
+        constexpr int R1 = NKS, R3 = NDB, NR = 2 * R1 + 2 * R3;
+        constexpr int EA = 16 / R1, EB = 16 / R3;
+        const int lim = qrow - k0 - 4 * h2;
+        f32x16 s0 = f32x16{}, s1 = f32x16{}, p0 = f32x16{}, p1 = f32x16{};
+        bf16x8 g0[2], g1[2];
+        auto fetch = [&](int k, bf16x8 (&o)[4]) {
+          if (k < 2 * R1) {
+            const int ks = k % R1, r0 = 32 * (k / R1);
+            o[0] = lo.rowk(Kt, r0, ks);
+            o[1] = lo.rowk(Vt, r0, ks);
+          } else if (k < NR) {
+            const int j = (k - 2 * R1) % R3, r0 = 32 * ((k - 2 * R1) / R3);
+            // two dQ MFMAs per region: steps st = 2 j, 2 j + 1 (s2 = st / NDB, db = st % NDB)
+            o[0] = lo.tr(Kt, r0 + 16 * ((2 * j) / NDB), (2 * j) % NDB);
+            o[2] = lo.tr(Kt, r0 + 16 * ((2 * j + 1) / NDB), (2 * j + 1) % NDB);
+          }
+        };
+        auto soft = [&](f32x16& sv, f32x16& dp, int kb, int r) {
+          float p = fexp2(fmaf(sv[r], scale_log2, -lse2));
+          if (MASK && crow(r, 0) > lim - 32 * kb) p = 0.f;
+          dp[r] = p * (dp[r] - dl);
+        };
+        bf16x8 cur[4], nxt[4];
+        fetch(0, cur);
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+          fetch(k + 1, nxt);
+          if (k < 2 * R1) {
+            const int ks = k % R1;
+            if (k < R1) {
+              s0 = mfma(cur[0], qf[ks], s0);
+              p0 = mfma(cur[1], df[ks], p0);
+            } else {
+              s1 = mfma(cur[0], qf[ks], s1);
+              p1 = mfma(cur[1], df[ks], p1);
+#pragma unroll
+              for (int e = 0; e < EA; ++e) soft(s0, p0, 0, (k - R1) * EA + e);
+              if (k == 2 * R1 - 1) { g0[0] = pack8(p0, 0); g0[1] = pack8(p0, 1); }
+            }
+          } else {
+            const int jj = k - 2 * R1, j = jj % R3;
+            const bool second = jj >= R3;
+            const int st0 = 2 * j, st1 = 2 * j + 1;
+            dqt[st0 % NDB] = mfma(cur[0], second ? g1[st0 / NDB] : g0[st0 / NDB], dqt[st0 % NDB]);
+            dqt[st1 % NDB] = mfma(cur[2], second ? g1[st1 / NDB] : g0[st1 / NDB], dqt[st1 % NDB]);
+            if (!second) {
+#pragma unroll
+              for (int e = 0; e < EB; ++e) soft(s1, p1, 1, j * EB + e);
+              if (j == R3 - 1) { g1[0] = pack8(p1, 0); g1[1] = pack8(p1, 1); }
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) cur[i] = nxt[i];
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      };
+      if (!CAUSAL || k0 + KT - 1 <= qw) tile(std::false_type{});
+      else if (k0 <= qw + 31) tile(std::true_type{});  // diagonal tile (else fully masked)
+    } else {
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
       const int kh = k0 + 32 * kb;
@@ -654,6 +911,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
         dqt[db] = mfma(kc, s2 ? d1 : d0, dqt[db]);
         kc = kn;
       }
+    }
     }
     __syncthreads();  // the DMA'd tile has landed (vmcnt(0)) and this tile is free
   };
@@ -710,6 +968,10 @@ hipError_t pra_attn_bwd(const void* q, const void* k, const void* v, const void*
   if (ldq % 8 || ldk % 8 || ldv % 8 || ldo % 8 || lddo % 8 || lddq % 4 || lddk % 4 || lddv % 4)
     return hipErrorInvalidValue;
   const float sl2 = scale * 1.4426950408889634f;
+  static const int bwd_prio = [] {
+    const char* e = getenv("PRA_ATTN_BWD_PRIO");
+    return e ? atoi(e) : 0;
+  }();
   {
     if (Hq > PRE_MAXH) return hipErrorInvalidValue;
     const int grid = B * (S / PRE_QB);
@@ -725,12 +987,28 @@ hipError_t pra_attn_bwd(const void* q, const void* k, const void* v, const void*
       const char* e = getenv("PRA_DKDV_NW");
       return e ? atoi(e) : 0;
     }();
+    // PRA_DKDV_IMPL: 1 = one-wave-per-SIMD pipelined kernel, 0 = two-wave kernel, unset = by loop
+    // length: the pipelined kernel pays a per-block prologue (64 KB of K/V) that only long query
+    // loops amortize (measured: S 8192 GQA 4:1 bwd 2.70 -> 2.03 ms; S 2048 MHA 1.30 -> 1.38 ms)
+    const char* impl_s = getenv("PRA_DKDV_IMPL");  // read per call (tests switch it)
+    const int impl_env = impl_s ? atoi(impl_s) : -1;
     const int nw = (nw_env == 4 || S % 256) ? 4 : 8;
+    const bool p2 = impl_env == 1 || (impl_env < 0 && (long)(Hq / Hkv) * S >= 8192);
+    if (p2 && nw_env == 0) {
+      dim3 g1((S / 128) * Hkv * B);
+#define LAUNCH1(DD, CC)                                                                                       \
+  hipLaunchKernelGGL((bwd_dkdv_p2_kernel<DD, CC>), g1, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,    \
+                     (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dk, (__bf16*)dv, S, Hq, Hkv, ldq, \
+                     ldk, ldv, lddo, lddk, lddv, scale, sl2)
+      if (D == 128) { if (causal) LAUNCH1(128, true); else LAUNCH1(128, false); }
+      else { if (causal) LAUNCH1(64, true); else LAUNCH1(64, false); }
+#undef LAUNCH1
+    } else {
     dim3 grid((S / (32 * nw)) * Hkv * B);
 #define LAUNCH(DD, CC, NWW)                                                                                     \
   hipLaunchKernelGGL((bwd_dkdv_kernel<DD, CC, NWW>), grid, dim3(NWW * 64), 0, st, (const __bf16*)q,             \
                      (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dk, (__bf16*)dv, \
-                     S, Hq, Hkv, ldq, ldk, ldv, lddo, lddk, lddv, scale, sl2)
+                     S, Hq, Hkv, ldq, ldk, ldv, lddo, lddk, lddv, scale, sl2, bwd_prio)
     if (nw == 8) {
       if (D == 128) { if (causal) LAUNCH(128, true, 8); else LAUNCH(128, false, 8); }
       else { if (causal) LAUNCH(64, true, 8); else LAUNCH(64, false, 8); }
@@ -739,6 +1017,7 @@ hipError_t pra_attn_bwd(const void* q, const void* k, const void* v, const void*
       else { if (causal) LAUNCH(64, true, 4); else LAUNCH(64, false, 4); }
     }
 #undef LAUNCH
+    }
   }
   {
     static const int dq_env = [] {
@@ -747,10 +1026,17 @@ hipError_t pra_attn_bwd(const void* q, const void* k, const void* v, const void*
     }();
     const int nwq = (dq_env == 4 || S % 256) ? 4 : 8;
     dim3 grid(((S + 32 * nwq - 1) / (32 * nwq)) * Hq * B);
+    const char* pipe_s = getenv("PRA_DQ_PIPE");  // read per call (tests switch it)
+    const bool pipe = pipe_s ? atoi(pipe_s) != 0 : true;
 #define LAUNCH(DD, CC, NWW)                                                                                     \
+  if (pipe)                                                                                                     \
+  hipLaunchKernelGGL((bwd_dq_kernel<DD, CC, NWW, true>), grid, dim3(NWW * 64), 0, st, (const __bf16*)q,         \
+                     (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dq, S, Hq, Hkv,  \
+                     ldq, ldk, ldv, lddo, lddq, scale, sl2, bwd_prio);                                            \
+  else                                                                                                          \
   hipLaunchKernelGGL((bwd_dq_kernel<DD, CC, NWW>), grid, dim3(NWW * 64), 0, st, (const __bf16*)q,               \
                      (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dq, S, Hq, Hkv,  \
-                     ldq, ldk, ldv, lddo, lddq, scale, sl2)
+                     ldq, ldk, ldv, lddo, lddq, scale, sl2, bwd_prio)
     if (nwq == 8) {
       if (D == 128) { if (causal) LAUNCH(128, true, 8); else LAUNCH(128, false, 8); }
       else { if (causal) LAUNCH(64, true, 8); else LAUNCH(64, false, 8); }

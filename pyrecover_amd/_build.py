@@ -56,7 +56,9 @@ def _run(cmd):
 # Per-file code-generation flags. attention.hip: no NaN semantics for fmaxf (drops the canonicalising
 # v_max before every max on MFMA results) and no SLP packing of f32 adds (packed f32 VALU beside
 # MFMAs costs more issue cycles than the scalar form).
-EXTRA_FLAGS = {"attention.hip": ["-fno-honor-nans", "-fno-slp-vectorize"]}
+# -amdgpu-mfma-vgpr-form: the one-wave-per-SIMD backward kernel keeps its loop-carried dK/dV sums in
+# VGPRs; with AGPR-form MFMAs the compiler copies them between the two files around every step.
+EXTRA_FLAGS = {"attention.hip": ["-fno-honor-nans", "-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"]}
 
 
 def build(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:

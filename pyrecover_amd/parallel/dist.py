@@ -74,6 +74,18 @@ def gpu_index(lrank: int) -> int:
     return int(o) if o not in (None, "") else lrank
 
 
+def rccl_pg_options():
+    """Process-group options for RCCL: collectives on a high-priority HIP stream, so a bucket's
+    all-reduce workgroups are dispatched ahead of queued backward GEMM tiles and start together on
+    every rank instead of spinning behind compute. ``PYRECOVER_RCCL_HIGH_PRIORITY=0`` turns it off."""
+    if os.environ.get("PYRECOVER_RCCL_HIGH_PRIORITY", "1") != "1" or not hasattr(torch.distributed,
+                                                                                  "ProcessGroupNCCL"):
+        return None
+    opts = torch.distributed.ProcessGroupNCCL.Options()
+    opts.is_high_priority_stream = True
+    return opts
+
+
 def maybe_init_distributed(activate_distributed: bool, backend: Optional[str] = None,
                            timeout_s: float = 1800.0) -> Tuple[int, int]:
     """Returns (local_rank, world_size). Initializes the process group when a multi-process
@@ -100,6 +112,9 @@ def maybe_init_distributed(activate_distributed: bool, backend: Optional[str] = 
         kw = {}
         if backend == "nccl":
             kw["device_id"] = torch.device("cuda", gpu_index(lrank))
+            opts = rccl_pg_options()
+            if opts is not None:
+                kw["pg_options"] = opts
         torch.distributed.init_process_group(backend=backend, rank=rank, world_size=world,
                                              timeout=datetime.timedelta(seconds=timeout_s), **kw)
     _STATE.update(rank=rank, world=world, local_rank=lrank, initialized=True, backend=backend)

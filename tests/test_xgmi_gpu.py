@@ -33,3 +33,11 @@ def test_xgmi_allreduce_matches_process_group(cuda, tmp_path):
     assert torch.equal(a["params"], b["params"])
     c = _run(tmp_path, "xgmi", 29533, overlap=True)
     assert torch.equal(a["params"], c["params"])
+
+
+def test_rccl_process_group_with_high_priority_stream(cuda):
+    """The RCCL process-group options used by parallel/dist.py are accepted by this build."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "dist_workers", "rccl_single.py"), "29541"],
+                       env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0 and "rccl ok" in r.stdout, (r.stdout + r.stderr)[-4000:]
