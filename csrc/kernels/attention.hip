@@ -77,6 +77,31 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& x, int s) {
 }
 
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+// Row-per-lane epilogue of a 32 x (32 NDB) accumulator tile X^T (lane l32 holds row l32 of X, register r
+// of block db holds column 32 db + crow(r, h2)): v_permlane32_swap hands each half-wave the other's
+// 4-column group, so every lane stores 8 contiguous bf16 (16 B) per instruction instead of two
+// separate 8-B pieces (cdna guide T21: halves the store-issue tail). p = &X[row][0], values * f.
+// All 64 lanes must execute it (the swap); `ok` guards only the stores.
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)a) |
+         ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)b) << 16);
+}
+template <int NDB>
+__device__ __forceinline__ void store_rows16(const f32x16 (&acc)[NDB], float f, __bf16* p, bool ok, int h2) {
+#pragma unroll
+  for (int db = 0; db < NDB; ++db)
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int a = 8 * m, c = 8 * m + 4;  // register groups rr = 2m (A) and 2m + 1 (B)
+      const auto x0 = __builtin_amdgcn_permlane32_swap(pack_bf16x2(acc[db][c] * f, acc[db][c + 1] * f),
+                                                      pack_bf16x2(acc[db][a] * f, acc[db][a + 1] * f), false, false);
+      const auto x1 = __builtin_amdgcn_permlane32_swap(pack_bf16x2(acc[db][c + 2] * f, acc[db][c + 3] * f),
+                                                      pack_bf16x2(acc[db][a + 2] * f, acc[db][a + 3] * f), false, false);
+      if (ok)
+        *reinterpret_cast<uint4*>(p + 32 * db + 16 * m + 8 * (1 - h2)) = make_uint4(x0[0], x1[0], x0[1], x1[1]);
+    }
+}
+
 
 // lanes i and i^32 exchange through v_permlane32_swap (no LDS round trip)
 __device__ __forceinline__ float half_max(float x) {
@@ -311,19 +336,10 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_kernel(const __bf16* __restric
     if (kt + 1 < nkt) body(IC<1>{}, kt + 1);
   }
 
-  if (qrow < S) {
+  {
     const float inv = 1.f / l_i;
-    __bf16* op = O + ((long)b * S + qrow) * ldo + hq * D;
-#pragma unroll
-    for (int db = 0; db < NDB; ++db)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        bf16x4 w;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = (__bf16)(o[db][4 * rr + j] * inv);
-        *reinterpret_cast<bf16x4*>(op + db * 32 + 8 * rr + 4 * h2) = w;
-      }
-    if (h2 == 0) LSE[((long)b * Hq + hq) * S + qrow] = (m_i + __log2f(l_i)) * 0.69314718055994531f;
+    store_rows16<NDB>(o, inv, O + ((long)b * S + qrow) * ldo + hq * D, qrow < S, h2);
+    if (qrow < S && h2 == 0) LSE[((long)b * Hq + hq) * S + qrow] = (m_i + __log2f(l_i)) * 0.69314718055994531f;
   }
 }
 
@@ -536,21 +552,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
     __syncthreads();
   }
 
-  __bf16* dkp = dK + ((long)b * S + krow) * lddk + hk * D;
-  __bf16* dvp = dV + ((long)b * S + krow) * lddv + hk * D;
-#pragma unroll
-  for (int db = 0; db < NDB; ++db)
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      bf16x4 wk, wv;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        wk[j] = (__bf16)(dkt[db][4 * rr + j] * scale);
-        wv[j] = (__bf16)(dvt[db][4 * rr + j]);
-      }
-      *reinterpret_cast<bf16x4*>(dkp + db * 32 + 8 * rr + 4 * h2) = wk;
-      *reinterpret_cast<bf16x4*>(dvp + db * 32 + 8 * rr + 4 * h2) = wv;
-    }
+  store_rows16<NDB>(dkt, scale, dK + ((long)b * S + krow) * lddk + hk * D, true, h2);
+  store_rows16<NDB>(dvt, 1.f, dV + ((long)b * S + krow) * lddv + hk * D, true, h2);
 }
 
 // ======================================================================================
@@ -718,21 +721,8 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_p2_kernel(
   }
 
   const int krow = kw + l32;
-  __bf16* dkp = dK + ((long)b * S + krow) * lddk + hk * D;
-  __bf16* dvp = dV + ((long)b * S + krow) * lddv + hk * D;
-#pragma unroll
-  for (int db = 0; db < NDB; ++db)
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      bf16x4 wk, wv;
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        wk[jj] = (__bf16)(dkt[db][4 * rr + jj] * scale);
-        wv[jj] = (__bf16)(dvt[db][4 * rr + jj]);
-      }
-      *reinterpret_cast<bf16x4*>(dkp + db * 32 + 8 * rr + 4 * h2) = wk;
-      *reinterpret_cast<bf16x4*>(dvp + db * 32 + 8 * rr + 4 * h2) = wv;
-    }
+  store_rows16<NDB>(dkt, scale, dK + ((long)b * S + krow) * lddk + hk * D, true, h2);
+  store_rows16<NDB>(dvt, 1.f, dV + ((long)b * S + krow) * lddv + hk * D, true, h2);
 }
 
 // ======================================================================================
@@ -920,18 +910,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
     if (kt + 1 < nkt) body(IC<1>{}, kt + 1);
   }
 
-  if (qrow < S) {
-    __bf16* dqp = dQ + ((long)b * S + qrow) * lddq + hq * D;
-#pragma unroll
-    for (int db = 0; db < NDB; ++db)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        bf16x4 w;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = (__bf16)(dqt[db][4 * rr + j] * scale);
-        *reinterpret_cast<bf16x4*>(dqp + db * 32 + 8 * rr + 4 * h2) = w;
-      }
-  }
+  store_rows16<NDB>(dqt, scale, dQ + ((long)b * S + qrow) * lddq + hq * D, qrow < S, h2);
 }
 
 }  // namespace attn
@@ -946,7 +925,7 @@ hipError_t pra_attn_fwd(const void* q, const void* k, const void* v, void* o, fl
                         int Hkv, int D, long ldq, long ldk, long ldv, long ldo, float scale, int causal,
                         hipStream_t st) {
   if (S % 64 || (D != 64 && D != 128) || Hq % Hkv) return hipErrorInvalidValue;
-  if (ldq % 8 || ldk % 8 || ldv % 8 || ldo % 4) return hipErrorInvalidValue;
+  if (ldq % 8 || ldk % 8 || ldv % 8 || ldo % 8) return hipErrorInvalidValue;
   constexpr int NW = 8;
   const int nqt = (S + 32 * NW - 1) / (32 * NW);
   dim3 grid(nqt * Hq * B), block(NW * 64);
@@ -965,7 +944,7 @@ hipError_t pra_attn_bwd(const void* q, const void* k, const void* v, const void*
                         int D, long ldq, long ldk, long ldv, long ldo, long lddo, long lddq, long lddk, long lddv,
                         float scale, int causal, hipStream_t st) {
   if (S % 128 || (D != 64 && D != 128) || Hq % Hkv) return hipErrorInvalidValue;
-  if (ldq % 8 || ldk % 8 || ldv % 8 || ldo % 8 || lddo % 8 || lddq % 4 || lddk % 4 || lddv % 4)
+  if (ldq % 8 || ldk % 8 || ldv % 8 || ldo % 8 || lddo % 8 || lddq % 8 || lddk % 8 || lddv % 8)
     return hipErrorInvalidValue;
   const float sl2 = scale * 1.4426950408889634f;
   static const int bwd_prio = [] {
