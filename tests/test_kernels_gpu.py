@@ -188,7 +188,10 @@ def _qkv(cuda, B, S, Hq, Hkv, D, seed=0, scale=1.0):
 @pytest.mark.parametrize("B,S,Hq,Hkv,D", [(1, 256, 4, 4, 128), (2, 512, 8, 2, 128), (1, 384, 4, 1, 64),
                                           (1, 128, 2, 2, 64), (1, 192, 4, 2, 128)])
 @pytest.mark.parametrize("causal", [True, False])
-def test_attention_fwd(cuda, B, S, Hq, Hkv, D, causal):
+@pytest.mark.parametrize("pipe", ["0", "1"])
+def test_attention_fwd(cuda, monkeypatch, pipe, B, S, Hq, Hkv, D, causal):
+    """Both forward kernels (PRA_FWD_PIPE: fwd_kernel / cross-tile pipelined fwd_p_kernel)."""
+    monkeypatch.setenv("PRA_FWD_PIPE", pipe)
     C = _ext.native()
     _, q, k, v = _qkv(cuda, B, S, Hq, Hkv, D)
     scale = 1 / math.sqrt(D)
@@ -198,8 +201,10 @@ def test_attention_fwd(cuda, B, S, Hq, Hkv, D, causal):
     assert (lse - lse_ref).abs().max().item() < 1e-3
 
 
-def test_attention_fwd_rescale_spike(cuda):
+@pytest.mark.parametrize("pipe", ["0", "1"])
+def test_attention_fwd_rescale_spike(cuda, monkeypatch, pipe):
     """Forces the online-softmax running max to jump at a late key tile (rule 26)."""
+    monkeypatch.setenv("PRA_FWD_PIPE", pipe)
     C = _ext.native()
     B, S, H, D = 1, 512, 2, 128
     _, q, k, v = _qkv(cuda, B, S, H, H, D, seed=3)
