@@ -245,3 +245,49 @@ def test_time_aware_budgets_async_write_and_drain(monkeypatch):
     assert 24.0 < rem <= 25.0
     st.inflight_drain = rem
     assert st.threshold > base + 30.0 + 24.0
+
+
+def test_loss_csv_log_line_and_metrics_jsonl(tmp_path, caplog):
+    """--log-loss-to-csv (reference train.py:143-151, 277-280: <exp>_loss_log.csv with a Step,Loss header
+    and one row per step), the reference log-line format (train.py:289-291) and --metrics-jsonl; a
+    resumed run appends to the CSV instead of truncating it."""
+    import csv
+    import json
+    import logging
+
+    from pyrecover_amd.cli import get_args
+    from pyrecover_amd.trainer import train
+
+    jl = tmp_path / "m.jsonl"
+    base = ["--model-preset", "llama-micro", "--synthetic-data", "--sequence-length", "128", "--batch-size", "2",
+            "--checkpoint-dir", str(tmp_path), "--experiment_name", "e", "--checkpoint-frequency", "3",
+            "--model-dtype", "fp32", "--num-workers", "0", "--logging-frequency", "1", "--log-loss-to-csv",
+            "--metrics-jsonl", str(jl)]
+    with caplog.at_level(logging.INFO):
+        train(get_args(base + ["--training-steps", "3"]))
+    lines = [r.getMessage() for r in caplog.records if r.getMessage().startswith("Epoch: ")]
+    assert len(lines) == 3
+    fields = [f.split(":")[0].strip() for f in lines[0].split("|")]
+    assert fields[:7] == ["Epoch", "Step", "Loss", "Tokens per second", "Training tokens per second (%)", "MFU (%)",
+                          "TFLOPs"]
+    train(get_args(base + ["--training-steps", "5", "--resume-from-checkpoint", "latest"]))
+    rows = list(csv.reader(open(tmp_path / "e" / "e_loss_log.csv")))
+    assert rows[0] == ["Step", "Loss"]
+    assert [int(r[0]) for r in rows[1:]] == [1, 2, 3, 4, 5]
+    assert all(float(r[1]) == float(r[1]) for r in rows[1:])
+    recs = [json.loads(x) for x in open(jl)]
+    assert [r["step"] for r in recs][-2:] == [4, 5]
+
+
+def test_teardown_after_gloo_group():
+    """maybe_cleanup_distributed (reference dist_utils.py) on an initialized one-rank gloo group."""
+    import torch.distributed as dist
+
+    from pyrecover_amd.parallel import dist as D
+
+    port = 29000 + os.getpid() % 1000
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    assert D.get_world_size() == 1 and D.is_rank0()
+    D.maybe_cleanup_distributed()
+    assert not dist.is_initialized()
+    D.maybe_cleanup_distributed()  # no-op when nothing is initialized
