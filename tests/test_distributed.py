@@ -84,3 +84,40 @@ def test_ddp_resume_bit_exact(tmp_path):
         assert torch.equal(a["model"][k], b["model"][k]), k
     for i in a["optimizer"]["state"]:
         assert torch.equal(a["optimizer"]["state"][i]["exp_avg_sq"], b["optimizer"]["state"][i]["exp_avg_sq"])
+
+
+def _worker_slurm(rank, world, port, argv, out_dir, end_in_s):
+    """A rank started by srun: only SLURM_* variables (no torchrun env)."""
+    import time
+
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        os.environ.pop(k, None)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SLURM_PROCID=str(rank),
+                      SLURM_NTASKS=str(world), SLURM_LOCALID=str(rank), SLURM_JOB_ID="4242")
+    if end_in_s is not None:
+        os.environ["SLURM_JOB_END_TIME"] = str(time.time() + end_in_s)
+    else:
+        os.environ.pop("SLURM_JOB_END_TIME", None)
+    torch.set_num_threads(2)
+    from pyrecover_amd.cli import get_args
+    from pyrecover_amd.trainer import train
+
+    res = train(get_args(argv))
+    torch.save(res, os.path.join(out_dir, f"res_{rank}.pt"))
+
+
+def test_fake_slurm_two_ranks_timeaware_stop_and_resume(tmp_path):
+    """2 gloo ranks bootstrapped from fake SLURM variables (SLURM_PROCID/NTASKS/LOCALID) and
+    a SLURM_JOB_END_TIME 30 s away: both ranks agree to stop after step 1 (stop flag broadcast from rank
+    0), write the final sharded checkpoint, and a second fake-SLURM job resumes it to completion."""
+    ck = tmp_path / "ck"
+    argv = _argv(ck, 6, ["--distributed", "--use-torch-distributed-ckpt", "--timeaware-checkpointing",
+                         "--checkpoint-frequency", "-1"])
+    mp.spawn(_worker_slurm, args=(2, _free_port(), argv, str(tmp_path), 30.0), nprocs=2, join=True)
+    r0 = torch.load(tmp_path / "res_0.pt", weights_only=False)
+    r1 = torch.load(tmp_path / "res_1.pt", weights_only=False)
+    assert r0["stopped_early"] and r1["stopped_early"] and r0["step"] == r1["step"] == 1
+    assert (ck / "e" / "ckpt_1_final" / ".metadata").exists()
+    argv2 = _argv(ck, 3, ["--distributed", "--use-torch-distributed-ckpt", "--resume-from-checkpoint", "latest"])
+    mp.spawn(_worker_slurm, args=(2, _free_port(), argv2, str(tmp_path), None), nprocs=2, join=True)
+    assert torch.load(tmp_path / "res_0.pt", weights_only=False)["step"] == 3
