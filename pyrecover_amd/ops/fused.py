@@ -79,8 +79,10 @@ def _mm_into(slot, a, b, shape):
 # Weight gradients dW = dY^T X with K = tokens. hipBLASLt runs this GEMM ~25-30% faster when both
 # operands are K-contiguous ("TN": dYt [out, T] times Xt [in, T]^T) than on the row-major
 # activations, which is worth two bandwidth-bound HIP transposes for the large projections
-# (QKV, W1|W3, W2, output head; tools/gemm_bench.py --layouts). PYRECOVER_TN_WGRAD=0 disables it.
+# (QKV, output projection, W1|W3, W2, output head; tools/gemm_bench.py --layouts).
+# PYRECOVER_TN_WGRAD=0 disables it.
 TN_WGRAD = os.environ.get("PYRECOVER_TN_WGRAD", "1") == "1"
+TN_WGRAD_WO = TN_WGRAD and os.environ.get("PYRECOVER_TN_WGRAD_WO", "1") == "1"
 
 
 def _tn_ok(t):
@@ -294,7 +296,10 @@ class _AttentionBlock(torch.autograd.Function):
         # slot may be updated by the optimizer (overlapped with backward) on another stream.
         w_qkv_t, w_o_t = ctx.w_t if ctx.w_t is not None else (None, None)
         do = (torch.mm(dy2, w_o_t.t()) if w_o_t is not None else torch.mm(dy2, w_o)).view(B, S, Hq, D)
-        slot_o.mm_(dy2.t(), o2, tuple(w_o.shape))
+        if TN_WGRAD_WO:
+            _wgrad_into(slot_o, dy2, o2, tuple(w_o.shape))  # TN: 0.53 -> ~0.3 ms + two 50-us transposes
+        else:
+            slot_o.mm_(dy2.t(), o2, tuple(w_o.shape))
         dqkv = torch.empty_like(qkv)
         q = qkv[:, :nq].view(B, S, Hq, D)
         k = qkv[:, nq:nq + nk].view(B, S, Hkv, D)
