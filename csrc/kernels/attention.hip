@@ -766,7 +766,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
 // constants (lse*log2e, delta) arrive by LDS-DMA into a double buffer, issued one step ahead.
 // ======================================================================================
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, 1) void bwd_dkdv_p2_kernel(
+__global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
     const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ V,
     const __bf16* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
     __bf16* __restrict__ dK, __bf16* __restrict__ dV, int S, int Hq, int Hkv, long ldq, long ldk, long ldv,
@@ -1173,13 +1173,15 @@ hipError_t pra_attn_bwd(const void* q, const void* k, const void* v, const void*
       const char* e = getenv("PRA_DKDV_NW");
       return e ? atoi(e) : 0;
     }();
-    // PRA_DKDV_IMPL: 1 = one-wave-per-SIMD pipelined kernel, 0 = two-wave kernel, unset = by loop
-    // length: the pipelined kernel pays a per-block prologue (64 KB of K/V) that only long query
+    // PRA_DKDV_IMPL: 1 = one-wave-per-SIMD pipelined kernel, 0 = two-wave kernel, unset = by shape:
+    // at D = 128 the pipelined kernel pays a per-block prologue (64 KB of K/V) that only long query
     // loops amortize (measured: S 8192 GQA 4:1 bwd 2.70 -> 2.03 ms; S 2048 MHA 1.30 -> 1.38 ms)
     const char* impl_s = getenv("PRA_DKDV_IMPL");  // read per call (tests switch it)
     const int impl_env = impl_s ? atoi(impl_s) : -1;
     const int nw = (nw_env == 4 || S % 256) ? 4 : 8;
-    const bool p2 = impl_env == 1 || (impl_env < 0 && (long)(Hq / Hkv) * S >= 8192);
+    // D = 64: 64 KB of LDS and <= 256 VGPRs, so two blocks share a CU and hide each other's prologue
+    // (B16 S2048 H16: 0.74 -> 0.68 ms bwd)
+    const bool p2 = impl_env == 1 || (impl_env < 0 && (D == 64 || (long)(Hq / Hkv) * S >= 8192));
     if (p2 && nw_env == 0) {
       dim3 g1((S / 128) * Hkv * B);
 #define LAUNCH1(DD, CC)                                                                                       \
