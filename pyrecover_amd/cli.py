@@ -104,6 +104,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--stop-at-step", type=int, default=None,
                    help="simulate a preemption: write the final checkpoint at this step and exit (testing)")
     p.add_argument("--metrics-jsonl", type=str, default=None, help="append per-log-step metrics as JSON lines")
+    p.add_argument("--grad-accumulation-steps", type=int, default=1,
+                   help="micro-batches of the local batch per optimizer step (gradients summed in place; "
+                        "the all-reduce and the update run once, after the last micro-batch)")
+    p.add_argument("--activation-checkpointing", action="store_true",
+                   help="recompute each transformer block's forward during backward (saves activations)")
     p.add_argument("--gemm-tuning", choices=["auto", "off", "tune"], default="auto")
     p.add_argument("--peak-tflops", type=float, default=2500.0, help="MFU denominator (MI355X dense bf16)")
     return p

@@ -18,6 +18,7 @@ from typing import List, Optional, Sequence, Tuple
 
 import torch
 import torch.nn as nn
+import torch.utils.checkpoint
 
 from ..config import TransformerModelArgs
 from ..ops import fused as F
@@ -116,6 +117,7 @@ class Transformer(nn.Module):
         self.output = nn.Linear(model_args.dim, model_args.vocab_size, bias=False)
         self.register_buffer("rope_tab", rope_table(self.freqs_cis), persistent=False)
         self.flat: Optional[FlatParams] = None
+        self.activation_checkpointing = False  # train.py --activation-checkpointing
 
     def _precompute_freqs_cis(self) -> torch.Tensor:
         a = self.model_args
@@ -205,31 +207,45 @@ class Transformer(nn.Module):
             return F.add_layer_norm(x, delta, mod.weight, mod.bias, self._slot([mod.weight, mod.bias]), mod.eps)
         return F.add_rms_norm(x, delta, mod.weight, self._slot([mod.weight]), mod.eps)
 
+    def _block(self, layer, h, pending, B: int, S: int):
+        """One TransformerBlock (reference model.py:325-327): returns (residual stream, the MLP
+        output still to be added -- the add is fused into the next norm)."""
+        a = self.model_args
+        dims = (B, S, a.n_heads, a.kv_heads, a.head_dim, True)
+        at, ff = layer.attention, layer.feed_forward
+        if pending is None:
+            x, n1 = h, self._norm(layer.attention_norm, h, None)
+        else:
+            x, n1 = self._norm(layer.attention_norm, h, pending)
+        qkv_p = [at.wq.weight, at.wk.weight, at.wv.weight]
+        att = F.attention_block(n1, self._weight(qkv_p), self._weight([at.wo.weight]), self._slot(qkv_p),
+                                self._slot([at.wo.weight]), self.rope_tab, dims, qkv_p + [at.wo.weight],
+                                w_t=(self._weight_t(qkv_p), self._weight_t([at.wo.weight])))
+        x2, n2 = self._norm(layer.ffn_norm, x, att)
+        up = [ff.w1.weight, ff.w3.weight]
+        mlp = F.swiglu_mlp(n2, self._weight(up), self._weight([ff.w2.weight]), self._slot(up),
+                           self._slot([ff.w2.weight]), up + [ff.w2.weight],
+                           w_t=(self._weight_t(up), self._weight_t([ff.w2.weight])))
+        return x2, mlp
+
     def _trunk(self, tokens: torch.Tensor):
         a = self.model_args
         B, S = tokens.shape
         if S > a.seq_len:
             raise ValueError(f"sequence length {S} exceeds model seq_len {a.seq_len}")
-        dims = (B, S, a.n_heads, a.kv_heads, a.head_dim, True)
         emb = self.tok_embeddings.weight
         h = F.embedding(tokens, emb, self._slot([emb]))
         pending = None
+        recompute = self.activation_checkpointing and torch.is_grad_enabled()
         for layer in self.layers.values():
-            at, ff = layer.attention, layer.feed_forward
-            if pending is None:
-                x, n1 = h, self._norm(layer.attention_norm, h, None)
+            if recompute:
+                # keep only the block's inputs; its forward is re-run right before its backward
+                # (its weights are still un-updated then: a gradient bucket completes only after
+                # the lowest layer it covers has finished backward)
+                h, pending = torch.utils.checkpoint.checkpoint(self._block, layer, h, pending, B, S,
+                                                               use_reentrant=False)
             else:
-                x, n1 = self._norm(layer.attention_norm, h, pending)
-            qkv_p = [at.wq.weight, at.wk.weight, at.wv.weight]
-            att = F.attention_block(n1, self._weight(qkv_p), self._weight([at.wo.weight]), self._slot(qkv_p),
-                                    self._slot([at.wo.weight]), self.rope_tab, dims, qkv_p + [at.wo.weight],
-                                    w_t=(self._weight_t(qkv_p), self._weight_t([at.wo.weight])))
-            x2, n2 = self._norm(layer.ffn_norm, x, att)
-            up = [ff.w1.weight, ff.w3.weight]
-            mlp = F.swiglu_mlp(n2, self._weight(up), self._weight([ff.w2.weight]), self._slot(up),
-                               self._slot([ff.w2.weight]), up + [ff.w2.weight],
-                               w_t=(self._weight_t(up), self._weight_t([ff.w2.weight])))
-            h, pending = x2, mlp
+                h, pending = self._block(layer, h, pending, B, S)
         if pending is None:
             return self._norm(self.norm, h, None)
         _, nf = self._norm(self.norm, h, pending)

@@ -203,6 +203,15 @@ class FlatParams:
         if self.reducer is not None:
             self.reducer.reset()
 
+    def next_micro_batch(self):
+        """Start another backward into the SAME gradients (gradient accumulation): slots stay
+        written, so every producer adds; readiness counting and bucket state start over."""
+        for s in self.slots:
+            if not s.fused:
+                self._pending_unfused[s.index] = len(s.params)
+        if self.reducer is not None:
+            self.reducer.reset()
+
     def _make_hook(self, slot: GradSlot) -> Callable:
         def hook(p):
             left = self._pending_unfused.get(slot.index, len(slot.params)) - 1

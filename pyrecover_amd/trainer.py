@@ -119,7 +119,8 @@ def train(args):
     seq_len = args.sequence_length
     global_batch_size = int(args.batch_size)
     local_batch_size = max(global_batch_size // world_size, 1)
-    n_samples = args.batch_size * args.training_steps
+    accum = max(1, int(getattr(args, "grad_accumulation_steps", 1) or 1))
+    n_samples = args.batch_size * args.training_steps * accum
     preset = get_preset(args.model_preset)
     if args.synthetic_data:
         vocab = args.vocab_size or preset.vocab_size
@@ -131,6 +132,9 @@ def train(args):
         vocab = args.vocab_size or tokenizer.vocab_size
         pad_id = tokenizer.pad_token_id
     log_rank0(f"Global batch size: {global_batch_size}\nLocal batch size: {local_batch_size}")
+    if accum > 1:
+        log_rank0(f"Gradient accumulation: {accum} micro-batches per step "
+                  f"({global_batch_size * accum} sequences per optimizer step)")
     train_sampler = ResumableDistributedSampler(len(train_ds), num_replicas=world_size, rank=rank, shuffle=True,
                                                 seed=args.seed)
     train_collator = CollatorForCLM(seq_len, pad_id)
@@ -144,6 +148,7 @@ def train(args):
                               use_flash_attention=args.use_flash_attention)
     with set_default_dtype(model_dtype), torch.device(device):
         model = Transformer(model_config)
+    model.activation_checkpointing = bool(getattr(args, "activation_checkpointing", False))
     flat = model.flatten_()
     overlap = not (args.clip_grad or args.no_overlap_optimizer)
     reducer = None
@@ -154,18 +159,22 @@ def train(args):
         log_rank0(f"Gradient buckets: {reducer.num_buckets}, {sum(reducer.bucket_bytes()) / 2**30:.2f} GiB"
                   f"{' (RCCL all-reduce)' if is_dist else ''}")
     model.train()
-    optimizer = FlatAdamW(flat, lr=args.learning_rate, fused=args.fused_optimizer, grad_scale=1.0 / world_size)
+    # SUM all-reduce of `accum` summed micro-batch gradients: the mean is folded into the update
+    grad_scale = 1.0 / (world_size * accum)
+    optimizer = FlatAdamW(flat, lr=args.learning_rate, fused=args.fused_optimizer, grad_scale=grad_scale)
     if overlap:
         optimizer.enable_overlap(reducer)
         optimizer.pre_update_fences.append(ckcore.fence_all)
     lr_scheduler = build_lr_scheduler(optimizer, args.lr_warmup_steps)
     step_graph = None
-    if args.compile:
+    if args.compile and accum > 1:
+        log_rank0("--compile with --grad-accumulation-steps > 1: running eagerly")
+    elif args.compile:
         if use_cuda:
             from .graph import StepGraph
 
             pre = (lambda: setattr(optimizer, "grad_scale_dev",
-                                   _clip_coef(flat, args.grad_max_norm, 1.0 / world_size))) if args.clip_grad else None
+                                   _clip_coef(flat, args.grad_max_norm, grad_scale))) if args.clip_grad else None
             step_graph = StepGraph(model, optimizer, reducer, fences=[ckcore.fence_all], pre_step=pre)
             log_rank0(f"--compile: the training step is captured into a HIP graph after "
                       f"{args.compile_warmup_steps} eager steps and replayed (no Inductor/Triton)")
@@ -280,32 +289,43 @@ def train(args):
         if args.profile and args.profile_step_start <= train_step <= args.profile_step_end:
             torch.cuda.nvtx.range_push(f"step_{train_step}") if use_cuda else None
 
-        train_sampler.set_epoch(epoch)
-        try:
-            input_ids, labels = next(train_dl_iterator)
-        except StopIteration:
-            epoch += 1
+        micro = []
+        for _ in range(accum):
             train_sampler.set_epoch(epoch)
-            train_dl_iterator = iter(train_dl)
-            input_ids, labels = next(train_dl_iterator)
-        train_sampler.advance(input_ids.shape[0])
+            try:
+                input_ids, labels = next(train_dl_iterator)
+            except StopIteration:
+                epoch += 1
+                train_sampler.set_epoch(epoch)
+                train_dl_iterator = iter(train_dl)
+                input_ids, labels = next(train_dl_iterator)
+            train_sampler.advance(input_ids.shape[0])
 
-        ntokens_since_last_log += global_batch_size * seq_len
-        num_items_in_batch = labels.ne(-100).sum()
-        ntraining_tokens_since_last_log += int(num_items_in_batch) * world_size
-        input_ids = input_ids.to(device, non_blocking=True)
-        labels = labels.to(device, non_blocking=True)
+            ntokens_since_last_log += global_batch_size * seq_len
+            num_items_in_batch = labels.ne(-100).sum()
+            ntraining_tokens_since_last_log += int(num_items_in_batch) * world_size
+            micro.append((input_ids.to(device, non_blocking=True), labels.to(device, non_blocking=True)))
 
         if step_graph is not None and eager_steps_this_run >= args.compile_warmup_steps:
-            loss = step_graph.step(input_ids, labels)  # fences the snapshot before the replay
+            loss = step_graph.step(*micro[0])  # fences the snapshot before the replay
         else:
             optimizer.zero_grad()
-            loss = model(input_ids, labels=labels)
-            loss.backward()
+            loss = None
+            for m, (input_ids, labels) in enumerate(micro):
+                if m:
+                    flat.next_micro_batch()  # producers now add into the written gradients
+                if reducer is not None:
+                    # no communication (or overlapped update) until the last micro-batch
+                    reducer.enabled = m == accum - 1
+                lm = model(input_ids, labels=labels)
+                lm.backward()
+                loss = lm.detach() if loss is None else loss + lm.detach()
+            if accum > 1:
+                loss = loss / accum
             if reducer is not None:
                 reducer.finish()
             if args.clip_grad:
-                optimizer.grad_scale_dev = _clip_coef(flat, args.grad_max_norm, 1.0 / world_size)
+                optimizer.grad_scale_dev = _clip_coef(flat, args.grad_max_norm, grad_scale)
             ckcore.fence_all()  # an async snapshot must land before parameters change
             optimizer.step()
             eager_steps_this_run += 1

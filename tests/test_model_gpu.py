@@ -56,7 +56,7 @@ def test_model_grads_vs_fp32_reference(cuda, preset, over):
         assert rel < 5e-2, (n, rel)
 
 
-def _train_steps(cuda, overlap, steps=3, preset="llama-tiny", seed=0):
+def _train_steps(cuda, overlap, steps=3, preset="llama-tiny", seed=0, recompute=False):
     from pyrecover_amd.optim.adamw import FlatAdamW
     from pyrecover_amd.parallel.ddp import GradReducer
 
@@ -67,6 +67,7 @@ def _train_steps(cuda, overlap, steps=3, preset="llama-tiny", seed=0):
     with torch.device(cuda):
         m = Transformer(a)
     torch.set_default_dtype(prev)
+    m.activation_checkpointing = recompute
     flat = m.flatten_()
     red = GradReducer(flat, bucket_cap_mb=0.5, first_bucket_mb=0.25)
     opt = FlatAdamW(flat, lr=1e-3)
@@ -89,6 +90,45 @@ def test_overlapped_optimizer_is_bit_identical(cuda):
     p1, v1, _ = _train_steps(cuda, overlap=True)
     assert nb > 3
     assert torch.equal(p0, p1) and torch.equal(v0, v1)
+
+
+def test_activation_checkpointing_is_bit_identical(cuda):
+    """Recomputing each block in backward (with the overlapped per-bucket update running) gives
+    the same parameters and moments as keeping the activations."""
+    p0, v0, _ = _train_steps(cuda, overlap=True)
+    p1, v1, _ = _train_steps(cuda, overlap=True, recompute=True)
+    assert torch.equal(p0, p1) and torch.equal(v0, v1)
+
+
+def test_gradient_accumulation_matches_full_batch(cuda):
+    """Two micro-batches (the second backward adds into the bf16 flat gradients through the fused
+    producers; the reducer only runs after the last) sum to twice the full-batch gradient."""
+    from pyrecover_amd.parallel.ddp import GradReducer
+
+    torch.manual_seed(0)
+    a = get_preset("llama-tiny", seq_len=256)
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.bfloat16)
+    with torch.device(cuda):
+        m = Transformer(a)
+    torch.set_default_dtype(prev)
+    flat = m.flatten_()
+    red = GradReducer(flat, bucket_cap_mb=0.5, first_bucket_mb=0.25)
+    t = torch.randint(0, a.vocab_size, (4, 257), device=cuda)
+    flat.zero_grad()
+    m(t[:, :-1], labels=t[:, 1:]).backward()
+    red.finish()
+    full = flat.grad.float().clone()
+    flat.zero_grad()
+    for i in range(2):
+        if i:
+            flat.next_micro_batch()
+        red.enabled = i == 1
+        m(t[2 * i:2 * i + 2, :-1], labels=t[2 * i:2 * i + 2, 1:]).backward()
+    red.finish()
+    acc = flat.grad.float() / 2
+    rel = ((acc - full).norm() / full.norm()).item()
+    assert rel < 2e-2, rel
 
 
 def test_training_is_deterministic(cuda):
