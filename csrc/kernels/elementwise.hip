@@ -5,6 +5,9 @@
 // 256 CUs x 8 blocks, per the CDNA4 memory-bound recipe.
 #include "common.h"
 
+#include <cstdlib>
+#include <cstring>
+
 namespace pra {
 
 static inline int grid_for(size_t work_items, int block = 256) {
@@ -20,6 +23,13 @@ static inline int grid_for(size_t work_items, int block = 256) {
 // x points at the first rotated column of token 0; `ld` is the token row stride; the first
 // `ncols` columns of each row (q heads followed by k heads, head_dim D each) are rotated.
 // tab is float2[S][D/2] = (cos, sin). sign = -1 applies the inverse rotation (backward).
+// (a + ib) * (c + is) with the FMA placement spelled out, so every RoPE kernel (row-major,
+// transposing, register-tile) rounds identically whatever the compiler's contraction choices.
+__device__ __forceinline__ void rot_pair(float a, float b, float c, float s, float& o0, float& o1) {
+  o0 = __builtin_fmaf(a, c, -(b * s));
+  o1 = __builtin_fmaf(a, s, b * c);
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void rope_kernel(T* __restrict__ x, const float2* __restrict__ tab,
                                                    long ntok, int ld, int ncols, int D, int S,
@@ -42,8 +52,7 @@ __global__ __launch_bounds__(256) void rope_kernel(T* __restrict__ x, const floa
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float a = v[2 * k], b = v[2 * k + 1];
-      o[2 * k] = a * c[k] - b * s[k];
-      o[2 * k + 1] = a * s[k] + b * c[k];
+      rot_pair(a, b, c[k], s[k], o[2 * k], o[2 * k + 1]);
     }
     store8<T>(p, o);
   }
@@ -176,23 +185,63 @@ __global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ sr
 }
 
 // ---------------------------------------------------------------------------------------
+// Register transpose (default): one wave moves a 64x64 tile with no LDS and no barrier. Lane
+// (g = lane & 7, ch = lane >> 3) loads the 8x8 sub-block rows 8g..8g+7, cols 8ch..8ch+7 as
+// eight 16-B loads (each instruction: 8 rows x 128 contiguous bytes), transposes it in VGPRs
+// with 32 v_perm_b32, and writes eight 16-B stores (each instruction: 8 output rows x 128 B).
+// 128 B in flight per lane and no LDS bank conflicts (the LDS kernel above reads its tile
+// column-wise with 8-way conflicts, which caps it near HBM rate even in isolation).
+__device__ __forceinline__ void transpose8x8_b16(const uint4 (&in)[8], uint4 (&out)[8]) {
+  const uint32_t* a = reinterpret_cast<const uint32_t*>(in);
+  uint32_t* o = reinterpret_cast<uint32_t*>(out);
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const uint32_t sel = (m & 1) ? 0x07060302u : 0x05040100u;  // hi halves / lo halves
+#pragma unroll
+    for (int e = 0; e < 4; ++e)  // out row m, dword e = (in row 2e, in row 2e+1) at column m
+      o[m * 4 + e] = __builtin_amdgcn_perm(a[(2 * e + 1) * 4 + (m >> 1)], a[(2 * e) * 4 + (m >> 1)], sel);
+  }
+}
+
+__global__ __launch_bounds__(256) void transpose_reg_kernel(const uint16_t* __restrict__ src,
+                                                            uint16_t* __restrict__ dst, long ld_src,
+                                                            long ld_dst, int tiles_c, long n_tiles) {
+  const long tile = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tile >= n_tiles) return;
+  const long r0 = (tile / tiles_c) * 64, c0 = (tile % tiles_c) * 64;
+  const int lane = threadIdx.x & 63, g = lane & 7, ch = lane >> 3;
+  const uint16_t* s = src + (r0 + 8 * g) * ld_src + c0 + 8 * ch;
+  uint4 in[8], out[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) in[k] = *reinterpret_cast<const uint4*>(s + k * ld_src);
+  transpose8x8_b16(in, out);
+  uint16_t* d = dst + (c0 + 8 * ch) * ld_dst + r0 + 8 * g;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) *reinterpret_cast<uint4*>(d + m * ld_dst) = out[m];
+}
+
+// ---------------------------------------------------------------------------------------
 // Transposing epilogues. The weight-gradient GEMM wants dY^T (K = tokens contiguous, see
 // transpose_kernel); the two producers of the largest dY's write it directly, in the same pass
 // that writes the row-major result (needed by the data-gradient GEMM):
 //   swiglu_bwd_t: dgu = [dg | du] (in place over gu) and dguT = dgu^T        (W1|W3 weight grad)
 //   rope_t:       x = inverse-RoPE(x) on the q|k columns (in place), xT = x^T (QKV weight grad)
-// Block = 64 tokens x 64 columns; values go through an LDS tile to 16-B transposed stores.
+// Block = 64 tokens x 64 columns; values go through an LDS tile to 16-B transposed stores. The
+// tile's 16-B chunks are XOR-swizzled by (row >> 3) so the column-wise reads are conflict-free.
 __device__ __forceinline__ void store_tile_t(uint16_t (*tile)[72], uint16_t* dst, long ld_dst, long c0, long t0) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int idx = threadIdx.x + 256 * i, rg = idx & 7, c = idx >> 3;
+    const int pc = (((c >> 3) ^ rg) << 3) | (c & 7);  // swizzled column (rows rg*8.. have r >> 3 == rg)
     uint32_t w[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      w[j] = (uint32_t)tile[rg * 8 + 2 * j][c] | ((uint32_t)tile[rg * 8 + 2 * j + 1][c] << 16);
+      w[j] = (uint32_t)tile[rg * 8 + 2 * j][pc] | ((uint32_t)tile[rg * 8 + 2 * j + 1][pc] << 16);
     *reinterpret_cast<uint4*>(dst + (c0 + c) * ld_dst + t0 + rg * 8) = make_uint4(w[0], w[1], w[2], w[3]);
   }
 }
+
+__device__ __forceinline__ int swz(int r, int ch) { return ch ^ ((r >> 3) & 7); }
 
 template <typename T>
 __device__ __forceinline__ void put8(uint16_t* row, const float* v) {
@@ -221,7 +270,7 @@ __global__ __launch_bounds__(256) void swiglu_fwd_t_kernel(const T* __restrict__
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = rnd<T>(silu_f(gv[j])) * uv[j];  // identical to swiglu_fwd_kernel
     store8<T>(a + t * lda + col, o);
-    put8<T>(&ta[r][ch * 8], o);
+    put8<T>(&ta[r][swz(r, ch) * 8], o);
   }
   __syncthreads();
   store_tile_t(ta, reinterpret_cast<uint16_t*>(aT), ntok, c0, t0);
@@ -252,8 +301,8 @@ __global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(const T* __restrict__
     }
     store8<T>(gu + t * ldgu + col, og);
     store8<T>(gu + t * ldgu + F + col, ou);
-    put8<T>(&tg[r][ch * 8], og);
-    put8<T>(&tu[r][ch * 8], ou);
+    put8<T>(&tg[r][swz(r, ch) * 8], og);
+    put8<T>(&tu[r][swz(r, ch) * 8], ou);
   }
   __syncthreads();
   store_tile_t(tg, reinterpret_cast<uint16_t*>(guT), ntok, c0, t0);
@@ -284,20 +333,175 @@ __global__ __launch_bounds__(256) void rope_t_kernel(T* x, T* __restrict__ xT, c
       float o[8];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        o[2 * k] = v[2 * k] * c[k] - v[2 * k + 1] * sn[k];
-        o[2 * k + 1] = v[2 * k] * sn[k] + v[2 * k + 1] * c[k];
+        rot_pair(v[2 * k], v[2 * k + 1], c[k], sn[k], o[2 * k], o[2 * k + 1]);
       }
       store8<T>(p, o);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = o[j];
     }
-    put8<T>(&tile[r][ch * 8], v);
+    put8<T>(&tile[r][swz(r, ch) * 8], v);
   }
   __syncthreads();
   store_tile_t(tile, reinterpret_cast<uint16_t*>(xT), ntok, c0, t0);
 }
 
+// ---------------------------------------------------------------------------------------
+// Register-tile versions of the three transposing epilogues (default): one wave per 64-token x
+// 64-column tile, lane (g, ch) owns tokens 8g..8g+7 x columns 8ch..8ch+7, so its eight row
+// vectors are the 8x8 block the transposed store needs (transpose8x8_b16). No LDS, no barrier,
+// every operand's eight row loads issued before any math. Same math and rounding as above.
+template <typename T>
+__device__ __forceinline__ void unpack8(const uint4& w, float (&o)[8]) {
+  const T* e = reinterpret_cast<const T*>(&w);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = to_f<T>(e[j]);
+}
+
+template <typename T>
+__device__ __forceinline__ uint4 pack8(const float (&v)[8]) {
+  T tmp[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) tmp[j] = from_f<T>(v[j]);
+  return *reinterpret_cast<const uint4*>(tmp);
+}
+
+// tile of this wave (tiles_c column tiles per 64-token row of tiles); false past the end
+__device__ __forceinline__ bool wave_tile(int tiles_c, long n_tiles, long& t0, int& c0, int& g, int& ch) {
+  const long tile = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tile >= n_tiles) return false;
+  t0 = (tile / tiles_c) * 64;
+  c0 = (int)(tile % tiles_c) * 64;
+  g = threadIdx.x & 7;
+  ch = (threadIdx.x >> 3) & 7;
+  return true;
+}
+
+__device__ __forceinline__ void store_t_reg(const uint4 (&rows)[8], uint16_t* dst, long ld_dst, long c0, long t0,
+                                            int g, int ch) {
+  uint4 out[8];
+  transpose8x8_b16(rows, out);
+  uint16_t* d = dst + (c0 + 8 * ch) * ld_dst + t0 + 8 * g;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) *reinterpret_cast<uint4*>(d + m * ld_dst) = out[m];
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_fwd_t_reg_kernel(const T* __restrict__ gu, T* __restrict__ a,
+                                                               T* __restrict__ aT, int F, int ldgu, int lda,
+                                                               long ntok, long n_tiles) {
+  long t0;
+  int c0, g, ch;
+  if (!wave_tile(F / 64, n_tiles, t0, c0, g, ch)) return;
+  const int col = c0 + 8 * ch;
+  uint4 G[8], U[8], A[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const T* row = gu + (t0 + 8 * g + k) * ldgu + col;
+    G[k] = *reinterpret_cast<const uint4*>(row);
+    U[k] = *reinterpret_cast<const uint4*>(row + F);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float gv[8], uv[8], o[8];
+    unpack8<T>(G[k], gv);
+    unpack8<T>(U[k], uv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = rnd<T>(silu_f(gv[j])) * uv[j];
+    A[k] = pack8<T>(o);
+    *reinterpret_cast<uint4*>(a + (t0 + 8 * g + k) * lda + col) = A[k];
+  }
+  store_t_reg(A, reinterpret_cast<uint16_t*>(aT), ntok, c0, t0, g, ch);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_bwd_t_reg_kernel(const T* __restrict__ dy, T* gu, T* __restrict__ guT,
+                                                               int F, int ldgu, int lddy, long ntok, long n_tiles) {
+  long t0;
+  int c0, g, ch;
+  if (!wave_tile(F / 64, n_tiles, t0, c0, g, ch)) return;
+  const int col = c0 + 8 * ch;
+  uint4 G[8], U[8], DY[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const long t = t0 + 8 * g + k;
+    G[k] = *reinterpret_cast<const uint4*>(gu + t * ldgu + col);
+    U[k] = *reinterpret_cast<const uint4*>(gu + t * ldgu + F + col);
+    DY[k] = *reinterpret_cast<const uint4*>(dy + t * lddy + col);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float gv[8], uv[8], dv[8], og[8], ou[8];
+    unpack8<T>(G[k], gv);
+    unpack8<T>(U[k], uv);
+    unpack8<T>(DY[k], dv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float sg = 1.f / (1.f + __expf(-gv[j]));
+      const float av = rnd<T>(gv[j] * sg);
+      const float da = rnd<T>(dv[j] * uv[j]);
+      ou[j] = dv[j] * av;
+      og[j] = da * sg * (1.f + gv[j] * (1.f - sg));
+    }
+    G[k] = pack8<T>(og);  // G/U now hold dg/du
+    U[k] = pack8<T>(ou);
+    const long t = t0 + 8 * g + k;
+    *reinterpret_cast<uint4*>(gu + t * ldgu + col) = G[k];
+    *reinterpret_cast<uint4*>(gu + t * ldgu + F + col) = U[k];
+  }
+  store_t_reg(G, reinterpret_cast<uint16_t*>(guT), ntok, c0, t0, g, ch);
+  store_t_reg(U, reinterpret_cast<uint16_t*>(guT), ntok, F + c0, t0, g, ch);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void rope_t_reg_kernel(T* x, T* __restrict__ xT, const float2* __restrict__ tab,
+                                                         int ld, int ncols, int nrot, int D, int S, float sign,
+                                                         long ntok, long n_tiles) {
+  long t0;
+  int c0, g, ch;
+  if (!wave_tile(ncols / 64, n_tiles, t0, c0, g, ch)) return;
+  const int col = c0 + 8 * ch;
+  uint4 X[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) X[k] = *reinterpret_cast<const uint4*>(x + (t0 + 8 * g + k) * ld + col);
+  if (col < nrot) {  // same math as rope_kernel
+    const int pi = (col % D) / 2;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const long t = t0 + 8 * g + k;
+      const float4* tp = reinterpret_cast<const float4*>(tab + (size_t)(t % S) * (D / 2) + pi);
+      const float4 cs01 = tp[0], cs23 = tp[1];
+      const float c[4] = {cs01.x, cs01.z, cs23.x, cs23.z};
+      const float sn[4] = {cs01.y * sign, cs01.w * sign, cs23.y * sign, cs23.w * sign};
+      float v[8], o[8];
+      unpack8<T>(X[k], v);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        rot_pair(v[2 * q], v[2 * q + 1], c[q], sn[q], o[2 * q], o[2 * q + 1]);
+      }
+      X[k] = pack8<T>(o);
+      *reinterpret_cast<uint4*>(x + t * ld + col) = X[k];
+    }
+  }
+  store_t_reg(X, reinterpret_cast<uint16_t*>(xT), ntok, c0, t0, g, ch);
+}
+
 }  // namespace pra
+
+// Which transpose / transposing-epilogue kernels run: by default the register-tile kernels, except
+// swiglu_bwd_t, whose register version (3 operands x 8 rows in flight) loses occupancy and
+// measured ~10% slower than the LDS one (tools/transpose_bench.py, profiles/transpose_ab_s2.log).
+// PYRECOVER_TRANSPOSE=lds / =reg forces one family everywhere (A/B).
+static int pra_transpose_mode() {  // 0 default, 1 lds, 2 reg
+  static const int v = [] {
+    const char* e = getenv("PYRECOVER_TRANSPOSE");
+    if (e && strcmp(e, "lds") == 0) return 1;
+    if (e && strcmp(e, "reg") == 0) return 2;
+    return 0;
+  }();
+  return v;
+}
+static bool pra_use_lds_transpose() { return pra_transpose_mode() == 1; }
+static bool pra_use_lds_swiglu_bwd_t() { return pra_transpose_mode() != 2; }
 
 extern "C" {
 
@@ -354,9 +558,15 @@ hipError_t pra_embedding_bwd(int dtype, const int64_t* sorted_ids, const int64_t
 
 hipError_t pra_transpose16(const void* src, void* dst, long R, long C, long ld_src, long ld_dst, hipStream_t s) {
   if (R % 64 || C % 64 || ld_src % 8 || ld_dst % 8) return hipErrorInvalidValue;
-  dim3 grid((unsigned)(C / 64), (unsigned)(R / 64));
-  hipLaunchKernelGGL((pra::transpose_kernel<uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)src, (uint16_t*)dst,
-                     ld_src, ld_dst);
+  if (pra_use_lds_transpose()) {
+    dim3 grid((unsigned)(C / 64), (unsigned)(R / 64));
+    hipLaunchKernelGGL((pra::transpose_kernel<uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)src,
+                       (uint16_t*)dst, ld_src, ld_dst);
+  } else {
+    const long n_tiles = (R / 64) * (C / 64);
+    hipLaunchKernelGGL(pra::transpose_reg_kernel, dim3((unsigned)((n_tiles + 3) / 4)), dim3(256), 0, s,
+                       (const uint16_t*)src, (uint16_t*)dst, ld_src, ld_dst, (int)(C / 64), n_tiles);
+  }
   return hipGetLastError();
 }
 
@@ -364,6 +574,14 @@ hipError_t pra_transpose16(const void* src, void* dst, long R, long C, long ld_s
 hipError_t pra_swiglu_fwd_t(int dtype, const void* gu, void* a, void* aT, long ntok, int F, int ldgu, int lda,
                             hipStream_t s) {
   if (ntok % 64 || F % 64 || ldgu % 8 || lda % 8) return hipErrorInvalidValue;
+  if (!pra_use_lds_transpose()) {
+    const long n_tiles = (ntok / 64) * (F / 64);
+    PRA_DISPATCH_16BIT(dtype, T,
+                       hipLaunchKernelGGL((pra::swiglu_fwd_t_reg_kernel<T>), dim3((unsigned)((n_tiles + 3) / 4)),
+                                          dim3(256), 0, s, (const T*)gu, (T*)a, (T*)aT, F, ldgu, lda, ntok,
+                                          n_tiles));
+    return hipGetLastError();
+  }
   dim3 grid((unsigned)(F / 64), (unsigned)(ntok / 64));
   PRA_DISPATCH_16BIT(dtype, T,
                      hipLaunchKernelGGL((pra::swiglu_fwd_t_kernel<T>), grid, dim3(256), 0, s, (const T*)gu, (T*)a,
@@ -375,6 +593,14 @@ hipError_t pra_swiglu_fwd_t(int dtype, const void* gu, void* a, void* aT, long n
 hipError_t pra_swiglu_bwd_t(int dtype, const void* dy, void* gu, void* guT, long ntok, int F, int ldgu, int lddy,
                             hipStream_t s) {
   if (ntok % 64 || F % 64 || ldgu % 8 || lddy % 8) return hipErrorInvalidValue;
+  if (!pra_use_lds_swiglu_bwd_t()) {
+    const long n_tiles = (ntok / 64) * (F / 64);
+    PRA_DISPATCH_16BIT(dtype, T,
+                       hipLaunchKernelGGL((pra::swiglu_bwd_t_reg_kernel<T>), dim3((unsigned)((n_tiles + 3) / 4)),
+                                          dim3(256), 0, s, (const T*)dy, (T*)gu, (T*)guT, F, ldgu, lddy, ntok,
+                                          n_tiles));
+    return hipGetLastError();
+  }
   dim3 grid((unsigned)(F / 64), (unsigned)(ntok / 64));
   PRA_DISPATCH_16BIT(dtype, T,
                      hipLaunchKernelGGL((pra::swiglu_bwd_t_kernel<T>), grid, dim3(256), 0, s, (const T*)dy, (T*)gu,
@@ -386,6 +612,14 @@ hipError_t pra_swiglu_bwd_t(int dtype, const void* dy, void* gu, void* guT, long
 hipError_t pra_rope_t(int dtype, void* x, void* xT, const void* tab, long ntok, int ld, int ncols, int nrot, int D,
                       int S, int inverse, hipStream_t s) {
   if (ntok % 64 || ncols % 64 || nrot % 8 || D % 8 || ld % 8) return hipErrorInvalidValue;
+  if (!pra_use_lds_transpose()) {
+    const long n_tiles = (ntok / 64) * (ncols / 64);
+    PRA_DISPATCH_16BIT(dtype, T,
+                       hipLaunchKernelGGL((pra::rope_t_reg_kernel<T>), dim3((unsigned)((n_tiles + 3) / 4)), dim3(256),
+                                          0, s, (T*)x, (T*)xT, (const float2*)tab, ld, ncols, nrot, D, S,
+                                          inverse ? -1.f : 1.f, ntok, n_tiles));
+    return hipGetLastError();
+  }
   dim3 grid((unsigned)(ncols / 64), (unsigned)(ntok / 64));
   PRA_DISPATCH_16BIT(dtype, T,
                      hipLaunchKernelGGL((pra::rope_t_kernel<T>), grid, dim3(256), 0, s, (T*)x, (T*)xT,

@@ -287,9 +287,9 @@ def test_transpose2d_exact(cuda, R, C):
     assert torch.equal(C_.transpose2d(xs), xs.t().contiguous())
 
 
-def test_swiglu_bwd_t_matches_swiglu_bwd_exactly(cuda):
+@pytest.mark.parametrize("T,F", [(256, 192), (64, 192), (2048, 1024)])
+def test_swiglu_bwd_t_matches_swiglu_bwd_exactly(cuda, T, F):
     C_ = _ext.native()
-    T, F = 256, 192
     gu = torch.randn(T, 2 * F, device=cuda).bfloat16()
     dy = torch.randn(T, F, device=cuda).bfloat16()
     ref = C_.swiglu_bwd(dy, gu.clone(), None)
@@ -299,9 +299,9 @@ def test_swiglu_bwd_t_matches_swiglu_bwd_exactly(cuda):
     assert torch.equal(guT, ref.t().contiguous())
 
 
-def test_swiglu_fwd_t_matches_swiglu_fwd_exactly(cuda):
+@pytest.mark.parametrize("T,F", [(256, 192), (64, 192), (2048, 1024)])
+def test_swiglu_fwd_t_matches_swiglu_fwd_exactly(cuda, T, F):
     C_ = _ext.native()
-    T, F = 256, 192
     gu = torch.randn(T, 2 * F, device=cuda).bfloat16()
     ref = C_.swiglu_fwd(gu)
     a, aT = C_.swiglu_fwd_t(gu)
