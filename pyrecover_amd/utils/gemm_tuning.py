@@ -30,6 +30,8 @@ def configure_gemm_tuning(mode: str = "auto", table: str = TABLE) -> bool:
         to.set_max_tuning_iterations(int(os.environ.get("PRA_TUNE_ITERS", "40")))
         # rank-specific output file is appended by torch when distributed; single-GPU tuning only
         to.set_filename(table, insert_device_ordinal=False)
+        if os.path.exists(table):  # extend an existing table: only new shapes are benchmarked
+            to.read_file(table)
         return True
     if not os.path.exists(table):
         return False
