@@ -14,6 +14,7 @@ after :meth:`Transformer.flatten_` all parameters/gradients live in flat buffers
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -170,7 +171,9 @@ class Transformer(nn.Module):
             self.flat = FlatParams(self.fusion_groups())
             # optimizer-state indices follow model.parameters() order, as in the reference
             self.flat.module_order = list(self.parameters())
-            for mats in self._gemm_weights():
+            # PRA_WEIGHT_SHADOWS=0 drops the transposed copies (dgrad GEMMs then read W as stored)
+            shadows = os.environ.get("PRA_WEIGHT_SHADOWS", "1") != "0"
+            for mats in self._gemm_weights() if shadows else []:
                 self.flat.register_transposed(mats, (sum(p.shape[0] for p in mats), mats[0].shape[1]))
             # parameters written through the module API must refresh the transposed shadows
             self.register_load_state_dict_post_hook(lambda mod, keys: mod.flat.refresh_transposed())
