@@ -29,7 +29,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="llama2-7b")
     ap.add_argument("--seq-len", type=int, default=2048)
-    ap.add_argument("--batch-per-gpu", type=int, default=8)
+    ap.add_argument("--batch-per-gpu", type=int, default=16)
     ap.add_argument("--bucket-mb", type=float, default=256.0)
     ap.add_argument("--lr", type=float, default=1e-5)
     ap.add_argument("--seed", type=int, default=1234)
