@@ -175,3 +175,29 @@ def test_transposed_weight_shadows_track_parameters(cuda):
     sd = {k: v.clone() * 0.5 for k, v in m.state_dict().items()}
     m.load_state_dict(sd)
     check()
+
+
+def test_weight_shadows_off_gives_the_same_gradients(cuda, monkeypatch):
+    """PRA_WEIGHT_SHADOWS=0 (data-gradient GEMMs read W as stored) matches the shadowed path up to
+    GEMM rounding."""
+    grads = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("PRA_WEIGHT_SHADOWS", flag)
+        torch.manual_seed(0)
+        a = get_preset("llama-tiny", seq_len=256)
+        prev = torch.get_default_dtype()
+        torch.set_default_dtype(torch.bfloat16)
+        with torch.device(cuda):
+            m = Transformer(a)
+        torch.set_default_dtype(prev)
+        flat = m.flatten_()
+        assert (flat.weight_t(m._gemm_weights()[0]) is None) == (flag == "0")
+        g = torch.Generator(device=cuda)
+        g.manual_seed(7)
+        t = torch.randint(0, a.vocab_size, (2, 257), device=cuda, generator=g)
+        flat.zero_grad()
+        m(t[:, :-1], labels=t[:, 1:]).backward()
+        torch.cuda.synchronize()
+        grads.append(flat.grad.float().clone())
+    rel = ((grads[0] - grads[1]).norm() / grads[0].norm()).item()
+    assert rel < 1e-2, rel
