@@ -10,6 +10,11 @@ update and LR-scheduler step -- nothing is skipped.
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it is launched by
 ``torch.distributed.run`` (one rank per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* from env).
 Rank 0 prints ONE JSON line; ``value`` is the whole-job aggregate tokens/s (max time over ranks).
+
+Started as ``python bench.py --gpus N`` (N>1) WITHOUT a rank environment, this process touches no
+GPU: it starts ``torch.distributed.run`` with N ranks as a child process on 127.0.0.1 and exits
+with its code. A rank whose process group does not have exactly N ranks exits non-zero, and the
+JSON line reports ``ranks_seen`` (the process group's size) next to ``n_gpus``.
 """
 from __future__ import annotations
 
@@ -42,13 +47,40 @@ def parse():
                     help="capture the step into a HIP graph after the warmup steps (train.py --compile)")
     ap.add_argument("--phase-timing", action="store_true",
                     help="record device events around forward / backward / optimizer of each timed step")
+    ap.add_argument("--cpu", action="store_true",
+                    help="run on the CPU over gloo (tests of the launcher and the DDP path; not a benchmark)")
     ap.add_argument("--gemm-tuning", choices=["auto", "off", "tune"], default="auto",
                     help="hipBLASLt solution table (tuning/): auto = use the committed table if present")
     return ap.parse_args()
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_command(argv, gpus: int, env) -> list:
+    """The child command that runs this benchmark with ``gpus`` ranks, or [] when this process is
+    already a rank (a torchrun/SLURM environment) or ``gpus`` is 1."""
+    if gpus <= 1 or "WORLD_SIZE" in env or "SLURM_PROCID" in env and int(env.get("SLURM_NTASKS", "1")) > 1:
+        return []
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + list(argv)
+
+
 def main():
     args = parse()
+    cmd = launch_command(sys.argv[1:], args.gpus, os.environ)
+    if cmd:
+        # no GPU call has happened in this process: the ranks are fresh children
+        import subprocess
+
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        sys.exit(subprocess.call(cmd, env=env))
     root = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, root)
     from pyrecover_amd.utils.gemm_tuning import configure_gemm_tuning
@@ -67,10 +99,20 @@ def main():
         lrank, world = D.maybe_init_distributed(True)
     else:
         lrank, world = 0, 1
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    dev = torch.device("cuda", D.gpu_index(lrank))
-    torch.cuda.set_device(dev)
+    ranks_seen = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
+    if world != args.gpus or ranks_seen != args.gpus:
+        print(f"error: --gpus {args.gpus} but the job has WORLD_SIZE={world} "
+              f"(process group: {ranks_seen} ranks)", file=sys.stderr)
+        sys.exit(2)
+    if args.cpu:
+        dev = torch.device("cpu")
+    else:
+        dev = torch.device("cuda", D.gpu_index(lrank))
+        torch.cuda.set_device(dev)
+
+    def sync():
+        if dev.type == "cuda":
+            sync()
     rank = D.get_rank()
 
     cfg = get_preset(args.model, seq_len=args.seq_len)
@@ -100,7 +142,12 @@ def main():
     phases = []
     sg = None
     if args.graph:
-        from pyrecover_amd.graph import StepGraph
+        from pyrecover_amd.graph import StepGraph, capture_allowed
+
+        ok, why = capture_allowed(world)
+        if not ok:
+            print(f"error: --graph: {why}", file=sys.stderr)
+            sys.exit(2)
 
         sg = StepGraph(model, opt, reducer)
     n_eager = [0]
@@ -112,7 +159,7 @@ def main():
             sched.step()
             return loss
         n_eager[0] += 1
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if timed else None
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if timed and dev.type == "cuda" else None
         opt.zero_grad()
         if ev:
             ev[0].record()
@@ -132,21 +179,21 @@ def main():
 
     for _ in range(args.warmup):
         loss = step()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         torch.distributed.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        if args.profile_steps and i < args.profile_steps:
+        if args.profile_steps and i < args.profile_steps and dev.type == "cuda":
             torch.cuda.nvtx.range_push(f"step{i}")
         loss = step(timed=args.phase_timing)
-        if args.profile_steps and i < args.profile_steps:
+        if args.profile_steps and i < args.profile_steps and dev.type == "cuda":
             torch.cuda.nvtx.range_pop()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         torch.distributed.barrier()
-    torch.cuda.synchronize()
+    sync()
     dt = time.perf_counter() - t0
     dt_t = torch.tensor([dt], device=dev, dtype=torch.float64)
     if world > 1:
@@ -163,6 +210,7 @@ def main():
             "value": round(tps, 2),
             "unit": "tokens/s",
             "n_gpus": world,
+            "ranks_seen": ranks_seen,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1000 * dt / args.steps, 3),
@@ -170,17 +218,24 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
+            "device": "cpu (gloo test run, not a benchmark)" if dev.type == "cpu" else "MI355X",
             "data": "synthetic (uniform random token ids), random-init weights",
             "config": {"model": f"{args.model}-shape ({n_params / 1e9:.2f}B params)", "global_batch": B * world,
                        "seq_len": S, "parallelism": f"dp{world}", "batch_per_gpu": B,
                        "bucket_mb": args.bucket_mb if world > 1 else None,
-                       "allreduce": args.allreduce if world > 1 else None, "optimizer": "AdamW (flat fused HIP)" + ("" if args.no_overlap_optimizer else ", overlapped with backward")},
+                       "allreduce": (None if world == 1 else "xgmi" if args.allreduce == "xgmi" else
+                                     "rccl" if torch.distributed.get_backend() == "nccl" else
+                                     torch.distributed.get_backend()),
+                       "dist_backend": torch.distributed.get_backend() if world > 1 else None,
+                       "grad_buckets": reducer.num_buckets,
+                       "rccl_high_priority_stream": os.environ.get("PYRECOVER_RCCL_HIGH_PRIORITY", "1") == "1",
+                       "optimizer": "AdamW (flat fused HIP)" + ("" if args.no_overlap_optimizer else ", overlapped with backward")},
             "tokens_per_sec_per_gpu": round(tps / world, 2),
             "model_tflops_per_gpu": round(fpt * tps / world / 1e12, 2),
             "mfu_pct_vs_2.5PF": round(100 * fpt * tps / world / 2.5e15, 2),
             "final_loss": round(final_loss, 4),
-            "peak_mem_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1),
-            "gemm_table": bool(torch.cuda.tunable.is_enabled()),
+            "peak_mem_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if dev.type == "cuda" else None,
+            "gemm_table": bool(torch.cuda.tunable.is_enabled()) if dev.type == "cuda" else False,
             "hip_graph": bool(args.graph),
         }
         if phases:

@@ -19,7 +19,29 @@ outside the graph. Shapes are static (fixed batch and sequence length), as in th
 """
 from __future__ import annotations
 
+import os
+
 import torch
+
+
+def capture_allowed(world_size: int) -> tuple:
+    """Whether the step may be captured with ``world_size`` ranks: ``(ok, reason)``.
+
+    One rank: always. Several ranks: the backward's bucket all-reduces would be captured into the
+    graph. Gloo collectives run on the host and cannot be captured at all; RCCL collectives can be
+    captured, but replaying them has not been validated on a multi-GPU node, so capture stays off
+    unless ``PYRECOVER_GRAPH_COLLECTIVES=1`` opts in. Callers run the step eagerly otherwise."""
+    if world_size <= 1:
+        return True, ""
+    import torch.distributed as dist
+
+    backend = dist.get_backend() if dist.is_initialized() else None
+    if backend != "nccl":
+        return False, f"backend {backend!r} collectives cannot be captured into a HIP graph"
+    if os.environ.get("PYRECOVER_GRAPH_COLLECTIVES", "0") != "1":
+        return False, ("HIP-graph capture of RCCL collectives is not validated on multi-GPU runs "
+                       "(set PYRECOVER_GRAPH_COLLECTIVES=1 to capture them anyway)")
+    return True, ""
 
 
 class StepGraph:

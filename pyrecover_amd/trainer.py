@@ -170,7 +170,12 @@ def train(args):
     if args.compile and accum > 1:
         log_rank0("--compile with --grad-accumulation-steps > 1: running eagerly")
     elif args.compile:
-        if use_cuda:
+        from .graph import capture_allowed
+
+        cap_ok, cap_why = capture_allowed(world_size)
+        if not cap_ok:
+            log_rank0(f"--compile: running eagerly: {cap_why}")
+        elif use_cuda:
             from .graph import StepGraph
 
             pre = (lambda: setattr(optimizer, "grad_scale_dev",

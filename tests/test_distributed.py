@@ -121,3 +121,56 @@ def test_fake_slurm_two_ranks_timeaware_stop_and_resume(tmp_path):
     argv2 = _argv(ck, 3, ["--distributed", "--use-torch-distributed-ckpt", "--resume-from-checkpoint", "latest"])
     mp.spawn(_worker_slurm, args=(2, _free_port(), argv2, str(tmp_path), None), nprocs=2, join=True)
     assert torch.load(tmp_path / "res_0.pt", weights_only=False)["step"] == 3
+
+
+def _bench_json(out: str) -> dict:
+    import json
+
+    lines = [ln for ln in out.splitlines() if ln.startswith('{"metric"')]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_bench_self_spawns_ranks():
+    """`python bench.py --gpus 2` without a rank environment starts 2 ranks itself (no silent 1-GPU
+    number); the JSON line reports n_gpus == ranks_seen == 2."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "2"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--cpu", "--model",
+                        "llama-micro", "--seq-len", "64", "--batch-per-gpu", "2", "--steps", "2", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _bench_json(r.stdout)
+    assert out["n_gpus"] == 2 and out["ranks_seen"] == 2, out
+    assert out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 4
+    assert out["config"]["dist_backend"] == "gloo"
+
+
+def test_bench_rejects_world_mismatch():
+    """A rank environment whose world size differs from --gpus is an error, not a 1-GPU number."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()), OMP_NUM_THREADS="2")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--cpu", "--model",
+                        "llama-micro", "--seq-len", "64", "--batch-per-gpu", "2", "--steps", "1", "--warmup", "0"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert '"metric"' not in r.stdout
+
+
+def test_bench_launch_command():
+    import bench
+
+    cmd = bench.launch_command(["--gpus", "8", "--steps", "3"], 8, {})
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=8" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and cmd[-3:] == ["--gpus", "8", "--steps", "3"][-3:]
+    assert bench.launch_command(["--gpus", "8"], 8, {"WORLD_SIZE": "8"}) == []
+    assert bench.launch_command([], 1, {}) == []
+    assert bench.launch_command(["--gpus", "4"], 4, {"SLURM_PROCID": "0", "SLURM_NTASKS": "4"}) == []
