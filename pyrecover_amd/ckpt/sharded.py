@@ -121,7 +121,8 @@ def save_ckpt_distributed(model, optimizer, lr_scheduler=None, sampler=None, ste
     ck = core.Checkpointer.get(dev)
     staged = ck.stage({k: v[0] for k, v in mine.items()})
     wr_items, keep, order = [], [], []
-    for k in sorted(mine, key=lambda x: list(items).index(x)):
+    pos = {k: i for i, k in enumerate(items)}
+    for k in sorted(mine, key=pos.__getitem__):
         val = staged[k]
         if isinstance(val, torch.Tensor):
             recs, kp = plan_archive(val, "archive")
@@ -145,7 +146,9 @@ def save_ckpt_distributed(model, optimizer, lr_scheduler=None, sampler=None, ste
             meta_local.append((k, "bytes", None, None))
     pend = {"path": str(path), "rank": rank, "world": world, "fname": fname, "meta": meta_local, "items": items,
             "max_keep": max_keep, "distributed": is_distributed, "t0": time.perf_counter()}
-    ck.write(str(path / fname), wr_items, False, fsync, (staged, keep), None)
+    # the Job caches its result, so whoever drains the engine first (poll_all / wait_all / a later
+    # save) cannot take this shard's layout away from finalize_pending
+    pend["job"] = ck.write(str(path / fname), wr_items, False, fsync, (staged, keep), None)
     _PENDING.append(pend)
     if not async_save:
         finalize_pending()
@@ -162,12 +165,12 @@ def finalize_pending():
     write ``.metadata`` + manifest, drop ``.incomplete``, apply retention."""
     while _PENDING:
         pend = _PENDING.pop(0)
-        results = core.wait_all()
-        res = results[-1] if results else None
-        local = []
-        if res is not None:
-            for (k, kind, dt, shape), (off, ln) in zip(pend["meta"], res["items"]):
-                local.append((k, kind, dt, shape, pend["fname"], off, ln))
+        res = pend["job"].wait()
+        if len(res["items"]) != len(pend["meta"]):
+            raise RuntimeError(f"shard {pend['fname']} of {pend['path']}: {len(res['items'])} records written, "
+                               f"{len(pend['meta'])} expected")
+        local = [(k, kind, dt, shape, pend["fname"], off, ln)
+                 for (k, kind, dt, shape), (off, ln) in zip(pend["meta"], res["items"])]
         gathered = [local]
         if pend["distributed"]:
             gathered = [None] * pend["world"]
