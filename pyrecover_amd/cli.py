@@ -99,6 +99,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--resubmit", choices=["none", "requeue", "chain"], default="none",
                    help="after a time-aware final checkpoint, requeue/chain the SLURM job")
     p.add_argument("--resubmit-script", type=str, default=None)
+    p.add_argument("--max-resubmits", type=int, default=10,
+                   help="stop resubmitting after this many requeues (SLURM_RESTART_COUNT) / chained jobs")
     p.add_argument("--handle-signals", action="store_true",
                    help="SIGUSR1/SIGTERM trigger the time-aware final checkpoint (#SBATCH --signal=B:USR1@T)")
     p.add_argument("--stop-at-step", type=int, default=None,

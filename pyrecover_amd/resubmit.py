@@ -4,7 +4,8 @@ pyrecover/__init__.py:6).
 Two mechanisms, selected by :func:`setup_resubmission`:
 
 * ``requeue``: ``scontrol requeue $SLURM_JOB_ID`` (needs ``#SBATCH --requeue``); the job restarts
-  with the same script, which passes ``--resume-from-checkpoint=latest``;
+  with the same script, which passes ``--resume-from-checkpoint=latest``; the limit counts
+  ``SLURM_RESTART_COUNT``, which SLURM increments on every requeue;
 * ``chain``: ``sbatch --dependency=afterany:$SLURM_JOB_ID <script> <args>`` submits a successor
   that starts when this job ends.
 
@@ -48,7 +49,12 @@ def resubmit_command(cfg: ResubmitConfig, env=None) -> Optional[List[str]]:
     job = env.get("SLURM_JOB_ID")
     if cfg.mode == "none" or not job:
         return None
-    count = int(env.get("PYRECOVER_RESUBMIT_COUNT", "0"))
+    # requeue restarts the same job, and SLURM counts those restarts itself; chain submits a new
+    # job, which carries the count in its environment
+    if cfg.mode == "requeue":
+        count = int(env.get("SLURM_RESTART_COUNT", "0") or 0)
+    else:
+        count = int(env.get("PYRECOVER_RESUBMIT_COUNT", "0") or 0)
     if count >= cfg.max_resubmits:
         return None
     if cfg.mode == "requeue":

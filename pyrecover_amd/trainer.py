@@ -250,7 +250,8 @@ def train(args):
         log_rank0(f"SLURM_JOB_END_TIME: {stopper.end_time}")
     if args.resubmit != "none":
         resub.setup_resubmission(args.resubmit, args.resubmit_script,
-                                 [a for a in os.environ.get("PYRECOVER_SCRIPT_ARGS", "").split() if a])
+                                 [a for a in os.environ.get("PYRECOVER_SCRIPT_ARGS", "").split() if a],
+                                 max_resubmits=args.max_resubmits)
 
     # ---------------- resume (reference train.py:192-212) ----------------
     train_step = 0

@@ -15,9 +15,16 @@
 #   --profile-nsys (rocprofv3 on MI355X)
 # plus: --async-checkpoint, --resubmit=requeue|chain, --model-preset=NAME, --synthetic-data,
 #       --batch-size=N, --training-steps=N
+#       --checkpoint-dir=DIR, --max-resubmits=N
 # Fixes vs the reference: --sequence-length is passed with its flag name, the
 # distributed run uses one task per GPU, SIGUSR1 ahead of the limit triggers the final checkpoint.
+#
+# Preemption path: `--signal=B:USR1@120` delivers SIGUSR1 to THIS batch shell 120 s before the
+# limit. The shell runs srun in the background and waits on it; its trap forwards the signal to
+# srun, which relays it to every task, where train.py --handle-signals writes ckpt_<N>_final and
+# (with --resubmit) requeues the job. A requeued job sees SLURM_RESTART_COUNT > 0 and resumes.
 set -euo pipefail
+cd "${SLURM_SUBMIT_DIR:-.}"
 mkdir -p logs
 
 # ---- job end time for time-aware checkpointing (reference :29-47) ----
@@ -66,6 +73,8 @@ for arg in "$@"; do
     --synthetic-data) EXTRA+=(--synthetic-data) ;;
     --async-checkpoint) EXTRA+=(--async-checkpoint) ;;
     --resubmit=*) EXTRA+=(--resubmit "${arg#*=}" --resubmit-script "$0") ;;
+    --max-resubmits=*) EXTRA+=(--max-resubmits "${arg#*=}") ;;
+    --checkpoint-dir=*) EXTRA+=(--checkpoint-dir "${arg#*=}") ;;
     --profile-nsys|--profile-rocprof) PROFILE=1 ;;
     *) echo "unknown argument $arg"; exit 2 ;;
   esac
@@ -93,5 +102,24 @@ if [ "$PROFILE" -eq 1 ]; then
        "${CMD[@]}" --profile)
 fi
 echo "Running: ${CMD[*]}"
-# one task per GPU; SLURM_PROCID/SLURM_LOCALID select rank and device
-srun --kill-on-bad-exit=1 --gpus-per-task=1 --gpu-bind=closest "${CMD[@]}"
+# one task per GPU; SLURM_PROCID/SLURM_LOCALID select rank and device. srun runs in the
+# background so the trap below can forward SIGUSR1/SIGTERM while the shell waits.
+srun --kill-on-bad-exit=1 --gpus-per-task=1 --gpu-bind=closest "${CMD[@]}" &
+SRUN_PID=$!
+forward() {
+  echo "batch shell: received $1, forwarding to the job step (srun pid $SRUN_PID)"
+  kill -s "$1" "$SRUN_PID" 2>/dev/null || true
+}
+trap 'forward USR1' USR1
+trap 'forward TERM' TERM
+RC=0
+# `wait` returns early (status > 128) whenever a trapped signal arrives: keep waiting for srun
+while true; do
+  set +e
+  wait "$SRUN_PID"
+  RC=$?
+  set -e
+  if ! kill -0 "$SRUN_PID" 2>/dev/null; then break; fi
+done
+echo "job step exited with status $RC"
+exit "$RC"

@@ -136,7 +136,12 @@ def test_resubmit_commands():
     cmd = resubmit_command(ResubmitConfig("chain", "run.sh", ["--continue"]), env)
     assert cmd[:2] == ["sbatch", "--dependency=afterany:77"] and cmd[-2:] == ["run.sh", "--continue"]
     assert resubmit_command(ResubmitConfig("requeue"), {}) is None
+    # requeue counts SLURM's own restart counter (scontrol requeue never changes our variable)
     assert resubmit_command(ResubmitConfig("requeue", max_resubmits=2),
+                            {"SLURM_JOB_ID": "1", "SLURM_RESTART_COUNT": "2"}) is None
+    assert resubmit_command(ResubmitConfig("requeue", max_resubmits=2),
+                            {"SLURM_JOB_ID": "1", "SLURM_RESTART_COUNT": "1"}) == ["scontrol", "requeue", "1"]
+    assert resubmit_command(ResubmitConfig("chain", "r.sh", max_resubmits=2),
                             {"SLURM_JOB_ID": "1", "PYRECOVER_RESUBMIT_COUNT": "2"}) is None
 
 
