@@ -112,7 +112,7 @@ def main():
 
     def sync():
         if dev.type == "cuda":
-            sync()
+            torch.cuda.synchronize(dev)
     rank = D.get_rank()
 
     cfg = get_preset(args.model, seq_len=args.seq_len)

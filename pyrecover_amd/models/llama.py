@@ -74,6 +74,19 @@ class Attention(nn.Module):
         self.wo = nn.Linear(args.n_heads * self.head_dim, args.dim, bias=False)
         self.use_flash_attention = args.use_flash_attention  # accepted for CLI parity; HIP flash always used on GPU
 
+    def forward(self, x: torch.Tensor, freqs_cis: torch.Tensor) -> torch.Tensor:
+        """Standalone module forward with the reference signature (reference model.py:194-230):
+        QKV projections, RoPE from ``freqs_cis`` (complex [>=S, head_dim/2]), causal GQA
+        attention, output projection. Runs the same fused op as :class:`Transformer` (one QKV
+        GEMM, in-place RoPE, HIP flash attention); weight gradients accumulate into ``.grad``."""
+        B, S, _ = x.shape
+        qkv = [self.wq.weight, self.wk.weight, self.wv.weight]
+        tab = rope_table(freqs_cis[:S].to(x.device))
+        dims = (B, S, self.n_heads, self.n_kv_heads, self.head_dim, True)
+        return F.attention_block(x, torch.cat([w.detach() for w in qkv], 0), self.wo.weight.detach(),
+                                 F.UnflatSlot(qkv), F.UnflatSlot([self.wo.weight]), tab, dims,
+                                 qkv + [self.wo.weight])
+
 
 class FeedForward(nn.Module):
     def __init__(self, dim: int, hidden_dim: int, multiple_of: int, ffn_dim_multiplier: Optional[float]):
@@ -85,6 +98,12 @@ class FeedForward(nn.Module):
         self.w1 = nn.Linear(dim, hidden_dim, bias=False)
         self.w2 = nn.Linear(hidden_dim, dim, bias=False)
         self.w3 = nn.Linear(dim, hidden_dim, bias=False)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """w2(silu(w1 x) * w3 x) (reference model.py:268-269) as the fused W1|W3 GEMM + SwiGLU op."""
+        up = [self.w1.weight, self.w3.weight]
+        return F.swiglu_mlp(x, torch.cat([w.detach() for w in up], 0), self.w2.weight.detach(),
+                            F.UnflatSlot(up), F.UnflatSlot([self.w2.weight]), up + [self.w2.weight])
 
 
 class TransformerBlock(nn.Module):
@@ -98,6 +117,17 @@ class TransformerBlock(nn.Module):
         self.num_layers = args.n_layers
         self.attention_norm = make_norm(args, args.dim)
         self.ffn_norm = make_norm(args, args.dim)
+
+    def _norm(self, mod, x, delta):
+        if isinstance(mod, LayerNorm):
+            return F.add_layer_norm(x, delta, mod.weight, mod.bias, F.UnflatSlot([mod.weight, mod.bias]), mod.eps)
+        return F.add_rms_norm(x, delta, mod.weight, F.UnflatSlot([mod.weight]), mod.eps)
+
+    def forward(self, x: torch.Tensor, freqs_cis: torch.Tensor) -> torch.Tensor:
+        """h = x + attention(attention_norm(x)); out = h + feed_forward(ffn_norm(h))
+        (reference model.py:325-327); the first residual add is fused into ffn_norm."""
+        h, n2 = self._norm(self.ffn_norm, x, self.attention(self._norm(self.attention_norm, x, None), freqs_cis))
+        return h + self.feed_forward(n2)
 
 
 class Transformer(nn.Module):
