@@ -446,34 +446,65 @@ at::Tensor grad_norm(const at::Tensor& x, double max_norm, double pre_scale) {
 }
 
 // q/k/v/o views [B, S, H, D] with stride(3)==1, stride(2)==D, stride(0)==S*stride(1).
-void check_bshd(const at::Tensor& t, const char* name, int64_t B, int64_t S, int64_t H, int64_t D) {
+void check_bshd(const at::Tensor& t, const char* name, int64_t B, int64_t S, int64_t H, int64_t D,
+                at::ScalarType dtype) {
   TORCH_CHECK(t.dim() == 4 && t.size(0) == B && t.size(1) == S && t.size(2) == H && t.size(3) == D,
               "attention: ", name, " must be [B, S, H, D] = [", B, ", ", S, ", ", H, ", ", D, "], got ", t.sizes());
-  TORCH_CHECK(t.stride(3) == 1 && t.stride(2) == D && t.stride(0) == S * t.stride(1),
+  TORCH_CHECK(t.stride(3) == 1 && t.stride(2) == D && (S == 1 || t.stride(0) == S * t.stride(1)),
               "attention: ", name, " must have token-major layout with contiguous heads, strides ", t.strides());
-  TORCH_CHECK(t.scalar_type() == at::kBFloat16, "attention: ", name, " must be bf16");
+  TORCH_CHECK(t.scalar_type() == dtype, "attention: ", name, " must be ", dtype, " like q");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "attention: ", name, " must be 16-B aligned");
+}
+
+void check_attn_dtype(const at::Tensor& q) {
+  TORCH_CHECK(q.scalar_type() == at::kBFloat16 || q.scalar_type() == at::kHalf,
+              "attention: the HIP kernels take bf16 or fp16 (got ", q.scalar_type(),
+              "); fp32/fp64 models run the attention in torch (pyrecover_amd.ops.fused)");
+}
+
+// Sequences that do not tile (S % 64 forward, S % 128 backward) run on zero-padded copies of
+// length round_up(S, 128). Causal attention is exact on the padding as is: a real query never
+// sees a later (padded) key, and padded query rows carry dO = 0, so they add nothing to dK/dV.
+// Non-causal attention passes the real length as the key bound `skv` (keys >= skv are masked).
+constexpr int64_t kSeqPad = 128;
+int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+at::Tensor pad_seq(const at::Tensor& t, int64_t Sp) {
+  at::Tensor out = at::zeros({t.size(0), Sp, t.size(2), t.size(3)}, t.options());
+  out.narrow(1, 0, t.size(1)).copy_(t);
+  return out;
 }
 
 std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale,
                                  bool causal) {
   const Range range_("pyrecover::attn_fwd");
   check_dev(q, "q");
+  check_attn_dtype(q);
   const int64_t B = q.size(0), S = q.size(1), Hq = q.size(2), D = q.size(3), Hkv = k.size(2);
-  check_bshd(q, "q", B, S, Hq, D);
-  check_bshd(k, "k", B, S, Hkv, D);
-  check_bshd(v, "v", B, S, Hkv, D);
+  check_bshd(q, "q", B, S, Hq, D, q.scalar_type());
+  check_bshd(k, "k", B, S, Hkv, D, q.scalar_type());
+  check_bshd(v, "v", B, S, Hkv, D, q.scalar_type());
   same_dev(q, k, "k");
   same_dev(q, v, "v");
-  TORCH_CHECK(S % 64 == 0, "attention: seq_len must be a multiple of 64");
   TORCH_CHECK(D == 64 || D == 128, "attention: head_dim must be 64 or 128");
   TORCH_CHECK(Hq % Hkv == 0, "attention: n_heads must be a multiple of n_kv_heads");
+  TORCH_CHECK(S > 0 && (S % 64 == 0 || S <= (int64_t)INT32_MAX - kSeqPad), "attention: bad seq_len");
   const c10::DeviceGuard guard(q.device());
+  if (S % 64) {
+    const int64_t Sp = round_up(S, kSeqPad);
+    at::Tensor qp = pad_seq(q, Sp), kp = pad_seq(k, Sp), vp = pad_seq(v, Sp);
+    at::Tensor o = at::empty({B, Sp, Hq, D}, q.options());
+    at::Tensor lse = at::empty({B, Hq, Sp}, q.options().dtype(at::kFloat));
+    check(pra_attn_fwd(dt(q), qp.data_ptr(), kp.data_ptr(), vp.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
+                       (int)B, (int)Sp, (int)Hq, (int)Hkv, (int)D, qp.stride(1), kp.stride(1), vp.stride(1),
+                       o.stride(1), (float)scale, causal ? 1 : 0, (int)S, stream_of(q)),
+          "attn_fwd");
+    return {o.narrow(1, 0, S).contiguous(), lse.narrow(2, 0, S).contiguous()};
+  }
   at::Tensor o = at::empty({B, S, Hq, D}, q.options());
   at::Tensor lse = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
-  check(pra_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), (int)B, (int)S,
-                     (int)Hq, (int)Hkv, (int)D, q.stride(1), k.stride(1), v.stride(1), o.stride(1), (float)scale,
-                     causal ? 1 : 0, stream_of(q)),
+  check(pra_attn_fwd(dt(q), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), (int)B,
+                     (int)S, (int)Hq, (int)Hkv, (int)D, q.stride(1), k.stride(1), v.stride(1), o.stride(1),
+                     (float)scale, causal ? 1 : 0, (int)S, stream_of(q)),
         "attn_fwd");
   return {o, lse};
 }
@@ -484,25 +515,48 @@ void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, con
               bool causal) {
   const Range range_("pyrecover::attn_bwd");
   check_dev(q, "q");
+  check_attn_dtype(q);
   const int64_t B = q.size(0), S = q.size(1), Hq = q.size(2), D = q.size(3), Hkv = k.size(2);
-  check_bshd(q, "q", B, S, Hq, D);
-  check_bshd(k, "k", B, S, Hkv, D);
-  check_bshd(v, "v", B, S, Hkv, D);
-  check_bshd(o, "o", B, S, Hq, D);
-  check_bshd(dout, "dout", B, S, Hq, D);
-  check_bshd(dq, "dq", B, S, Hq, D);
-  check_bshd(dk, "dk", B, S, Hkv, D);
-  check_bshd(dv, "dv", B, S, Hkv, D);
-  TORCH_CHECK(S % 128 == 0, "attention backward: seq_len must be a multiple of 128");
+  const at::ScalarType ty = q.scalar_type();
+  check_bshd(q, "q", B, S, Hq, D, ty);
+  check_bshd(k, "k", B, S, Hkv, D, ty);
+  check_bshd(v, "v", B, S, Hkv, D, ty);
+  check_bshd(o, "o", B, S, Hq, D, ty);
+  check_bshd(dout, "dout", B, S, Hq, D, ty);
+  check_bshd(dq, "dq", B, S, Hq, D, ty);
+  check_bshd(dk, "dk", B, S, Hkv, D, ty);
+  check_bshd(dv, "dv", B, S, Hkv, D, ty);
   TORCH_CHECK(D == 64 || D == 128, "attention: head_dim must be 64 or 128");
+  TORCH_CHECK(Hq % Hkv == 0, "attention: n_heads must be a multiple of n_kv_heads");
   TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.numel() == B * Hq * S && lse.is_contiguous(), "attention: lse");
   for (const at::Tensor& t : {k, v, o, dout, lse, dq, dk, dv}) same_dev(q, t, "attention operand");
   const c10::DeviceGuard guard(q.device());
+  if (S % kSeqPad) {
+    const int64_t Sp = round_up(S, kSeqPad);
+    at::Tensor qp = pad_seq(q, Sp), kp = pad_seq(k, Sp), vp = pad_seq(v, Sp), op = pad_seq(o, Sp),
+               dop = pad_seq(dout, Sp);
+    // padded rows: any finite lse (their dO is zero)
+    at::Tensor lp = at::zeros({B, Hq, Sp}, lse.options());
+    lp.narrow(2, 0, S).copy_(lse.view({B, Hq, S}));
+    at::Tensor dqp = at::empty_like(qp), dkp = at::empty_like(kp), dvp = at::empty_like(vp);
+    at::Tensor delta = at::empty({B, Hq, Sp}, q.options().dtype(at::kFloat));
+    check(pra_attn_bwd(dt(q), qp.data_ptr(), kp.data_ptr(), vp.data_ptr(), op.data_ptr(), dop.data_ptr(),
+                       lp.data_ptr<float>(), delta.data_ptr<float>(), dqp.data_ptr(), dkp.data_ptr(), dvp.data_ptr(),
+                       (int)B, (int)Sp, (int)Hq, (int)Hkv, (int)D, qp.stride(1), kp.stride(1), vp.stride(1),
+                       op.stride(1), dop.stride(1), dqp.stride(1), dkp.stride(1), dvp.stride(1), (float)scale,
+                       causal ? 1 : 0, (int)S, stream_of(q)),
+          "attn_bwd");
+    dq.copy_(dqp.narrow(1, 0, S));
+    dk.copy_(dkp.narrow(1, 0, S));
+    dv.copy_(dvp.narrow(1, 0, S));
+    return;
+  }
   at::Tensor delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
-  check(pra_attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
-                     delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), (int)B, (int)S, (int)Hq,
-                     (int)Hkv, (int)D, q.stride(1), k.stride(1), v.stride(1), o.stride(1), dout.stride(1), dq.stride(1),
-                     dk.stride(1), dv.stride(1), (float)scale, causal ? 1 : 0, stream_of(q)),
+  check(pra_attn_bwd(dt(q), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
+                     lse.data_ptr<float>(), delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
+                     (int)B, (int)S, (int)Hq, (int)Hkv, (int)D, q.stride(1), k.stride(1), v.stride(1), o.stride(1),
+                     dout.stride(1), dq.stride(1), dk.stride(1), dv.stride(1), (float)scale, causal ? 1 : 0, (int)S,
+                     stream_of(q)),
         "attn_bwd");
 }
 

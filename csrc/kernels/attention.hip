@@ -1,4 +1,4 @@
-// Flash attention forward + deterministic backward for gfx950 (CDNA4), bf16, head_dim 64/128,
+// Flash attention forward + deterministic backward for gfx950 (CDNA4), bf16 or fp16, head_dim 64/128,
 // causal or full, native GQA (kv head = q head / (Hq/Hkv); no repeat_kv copies).
 //
 // Replaces the reference's SDPA / flash-attn call (reference model.py:179-230; N1/N2 in
@@ -57,10 +57,21 @@ __device__ __forceinline__ void lay_inverse(int o, int& r, int& ch) {  // byte o
   ch = 4 * sub + (slot ^ ((r >> 2) & 3));
 }
 
-__device__ __forceinline__ bf16x8 lds_read16(const __bf16* tile, int byte_off) {
-  return *reinterpret_cast<const bf16x8*>(reinterpret_cast<const char*>(tile) + byte_off);
+// Element traits: the kernels are instantiated for bf16 (v_mfma_f32_32x32x16_bf16) and fp16
+// (v_mfma_f32_32x32x16_f16); both move as 8 x 16-bit per lane and accumulate in fp32.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+template <typename T> struct Elem;
+template <> struct Elem<__bf16> { typedef bf16x8 v8; };
+template <> struct Elem<_Float16> { typedef f16x8 v8; };
+template <typename T>
+using V8 = typename Elem<T>::v8;
+
+template <typename T>
+__device__ __forceinline__ V8<T> lds_read16(const T* tile, int byte_off) {
+  return *reinterpret_cast<const V8<T>*>(reinterpret_cast<const char*>(tile) + byte_off);
 }
-__device__ __forceinline__ i16x4 tr4(const __bf16* tile, int byte_off) {
+template <typename T>
+__device__ __forceinline__ i16x4 tr4(const T* tile, int byte_off) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
       (lds_i16x4*)(reinterpret_cast<const char*>(tile) + byte_off));
 }
@@ -68,35 +79,39 @@ __device__ __forceinline__ i16x4 tr4(const __bf16* tile, int byte_off) {
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
+__device__ __forceinline__ f32x16 mfma(f16x8 a, f16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
 
-__device__ __forceinline__ bf16x8 pack8(const f32x16& x, int s) {
-  bf16x8 r;
+template <typename T>
+__device__ __forceinline__ V8<T> pack8(const f32x16& x, int s) {
+  V8<T> r;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (__bf16)x[8 * s + j];
+  for (int j = 0; j < 8; ++j) r[j] = (T)x[8 * s + j];
   return r;
 }
 
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 // Row-per-lane epilogue of a 32 x (32 NDB) accumulator tile X^T (lane l32 holds row l32 of X, register r
 // of block db holds column 32 db + crow(r, h2)): v_permlane32_swap hands each half-wave the other's
-// 4-column group, so every lane stores 8 contiguous bf16 (16 B) per instruction instead of two
+// 4-column group, so every lane stores 8 contiguous 16-bit values (16 B) per instruction instead of two
 // separate 8-B pieces (cdna guide T21: halves the store-issue tail). p = &X[row][0], values * f.
 // All 64 lanes must execute it (the swap); `ok` guards only the stores.
-__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
-  return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)a) |
-         ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)b) << 16);
+template <typename T>
+__device__ __forceinline__ uint32_t pack_x2(float a, float b) {
+  return (uint32_t)__builtin_bit_cast(uint16_t, (T)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (T)b) << 16);
 }
-template <int NDB>
-__device__ __forceinline__ void store_rows16(const f32x16 (&acc)[NDB], float f, __bf16* p, bool ok, int h2) {
+template <typename T, int NDB>
+__device__ __forceinline__ void store_rows16(const f32x16 (&acc)[NDB], float f, T* p, bool ok, int h2) {
 #pragma unroll
   for (int db = 0; db < NDB; ++db)
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
       const int a = 8 * m, c = 8 * m + 4;  // register groups rr = 2m (A) and 2m + 1 (B)
-      const auto x0 = __builtin_amdgcn_permlane32_swap(pack_bf16x2(acc[db][c] * f, acc[db][c + 1] * f),
-                                                      pack_bf16x2(acc[db][a] * f, acc[db][a + 1] * f), false, false);
-      const auto x1 = __builtin_amdgcn_permlane32_swap(pack_bf16x2(acc[db][c + 2] * f, acc[db][c + 3] * f),
-                                                      pack_bf16x2(acc[db][a + 2] * f, acc[db][a + 3] * f), false, false);
+      const auto x0 = __builtin_amdgcn_permlane32_swap(pack_x2<T>(acc[db][c] * f, acc[db][c + 1] * f),
+                                                      pack_x2<T>(acc[db][a] * f, acc[db][a + 1] * f), false, false);
+      const auto x1 = __builtin_amdgcn_permlane32_swap(pack_x2<T>(acc[db][c + 2] * f, acc[db][c + 3] * f),
+                                                      pack_x2<T>(acc[db][a + 2] * f, acc[db][a + 3] * f), false, false);
       if (ok)
         *reinterpret_cast<uint4*>(p + 32 * db + 16 * m + 8 * (1 - h2)) = make_uint4(x0[0], x1[0], x0[1], x1[1]);
     }
@@ -114,13 +129,13 @@ __device__ __forceinline__ float half_sum(float x) {
 }
 
 // Stage ROWS x D rows of a [.., ld]-strided bf16 tensor into registers (global loads only).
-template <int D, int ROWS, int NT = 256>
+template <typename T, int D, int ROWS, int NT = 256>
 struct Stage {
   static constexpr int CH = D / 8;
   static constexpr int CPT = (ROWS * CH + NT - 1) / NT;
   static constexpr bool EXACT = CPT * NT == ROWS * CH;  // else the last pass is partial
   uint4 r[CPT];
-  __device__ __forceinline__ void load(const __bf16* g, long ld, int row0, int nrows_valid) {
+  __device__ __forceinline__ void load(const T* g, long ld, int row0, int nrows_valid) {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       const int idx = i * NT + threadIdx.x;
@@ -132,7 +147,7 @@ struct Stage {
         r[i] = make_uint4(0, 0, 0, 0);
     }
   }
-  __device__ __forceinline__ void store(__bf16* tile) const {
+  __device__ __forceinline__ void store(T* tile) const {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       const int idx = i * NT + threadIdx.x;
@@ -147,7 +162,7 @@ struct Stage {
 // writes 1 KiB per wave-instruction linearly (base + 16 B * lane), so each lane fetches the
 // (row, chunk) that the image places at its linear position.
 // No VGPR staging; rows must be in bounds (callers guarantee S % tile == 0).
-template <int D, int ROWS, int NWV = 4>
+template <typename T, int D, int ROWS, int NWV = 4>
 struct GStage {
   static constexpr int CH = D / 8;
   static constexpr int NI = ROWS * CH / (NWV * 64);
@@ -162,7 +177,7 @@ struct GStage {
       off[i] = row * (int)ld + ch * 8;
     }
   }
-  __device__ __forceinline__ void issue(const __bf16* g, __bf16* tile) const {
+  __device__ __forceinline__ void issue(const T* g, T* tile) const {
     const int wid = threadIdx.x >> 6;
 #pragma unroll
     for (int i = 0; i < NI; ++i)
@@ -177,7 +192,7 @@ __device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2
 
 // Lane-constant LDS byte offsets of the MFMA operand reads (image above). For a row base r0 that
 // is a multiple of 16, everything else is a compile-time immediate on the ds_read.
-template <int D>
+template <typename T, int D>
 struct LaneOff {
   int re, ro;  // ds_read_b128 of row l32, chunk 2*ks + h2: even / odd ks
   int tl, th;  // ds_read_b64_tr_b16 blocks (rows +0..7 / +8..15) of the transposed 32x16 operand
@@ -192,13 +207,13 @@ struct LaneOff {
     th = lay_byte<D>(r + 8, ch) + 8 * (p & 1);
   }
   // transposed operand: rows [r0, r0+16) (r0 % 16 == 0), columns [32 db, 32 db + 32)
-  __device__ __forceinline__ bf16x8 tr(const __bf16* tile, int r0, int db) const {
+  __device__ __forceinline__ V8<T> tr(const T* tile, int r0, int db) const {
     const i16x4 lo = tr4(tile, r0 * 2 * D + 512 * db + tl);
     const i16x4 hi = tr4(tile, r0 * 2 * D + 512 * db + th);
-    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    return __builtin_bit_cast(V8<T>, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
   }
   // row operand: rows [r0, r0+32) (r0 % 16 == 0), k-step ks (columns 16 ks .. 16 ks + 15)
-  __device__ __forceinline__ bf16x8 rowk(const __bf16* tile, int r0, int ks) const {
+  __device__ __forceinline__ V8<T> rowk(const T* tile, int r0, int ks) const {
     return lds_read16(tile, r0 * 2 * D + 512 * (ks >> 1) + ((ks & 1) ? ro : re));
   }
 };
@@ -211,14 +226,14 @@ using IC = std::integral_constant<int, N>;
 // ======================================================================================
 // Block = NW waves x 32 query rows (NW = 8: one 512-thread block per CU, 2 waves per SIMD), so
 // each staged K/V tile feeds 8 waves' MFMAs.
-template <int D, bool CAUSAL, int NW>
-__global__ __launch_bounds__(NW * 64, 2) void fwd_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K,
-                                                         const __bf16* __restrict__ V, __bf16* __restrict__ O,
+template <typename T, int D, bool CAUSAL, int NW>
+__global__ __launch_bounds__(NW * 64, 2) void fwd_kernel(const T* __restrict__ Q, const T* __restrict__ K,
+                                                         const T* __restrict__ V, T* __restrict__ O,
                                                          float* __restrict__ LSE, int S, int Hq, int Hkv, long ldq,
-                                                         long ldk, long ldv, long ldo, float scale_log2) {
+                                                         long ldk, long ldv, long ldo, float scale_log2, int skv) {
   constexpr int KT = 64, QT = 32 * NW;
   constexpr int NKS = D / 16, NDB = D / 32, TILE = KT * D;
-  __shared__ __attribute__((aligned(16))) __bf16 smem[4 * TILE];  // K0 V0 K1 V1
+  __shared__ __attribute__((aligned(16))) T smem[4 * TILE];  // K0 V0 K1 V1
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h2 = lane >> 5, l32 = lane & 31;
   const int nqt = (S + QT - 1) / QT;
@@ -229,17 +244,17 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_kernel(const __bf16* __restric
   const int hk = hq / (Hq / Hkv);
   const int q0 = qt * QT, qw = q0 + wid * 32;
 
-  const __bf16* Qb = Q + (long)b * S * ldq + hq * D;
-  const __bf16* Kb = K + (long)b * S * ldk + hk * D;
-  const __bf16* Vb = V + (long)b * S * ldv + hk * D;
+  const T* Qb = Q + (long)b * S * ldq + hq * D;
+  const T* Kb = K + (long)b * S * ldk + hk * D;
+  const T* Vb = V + (long)b * S * ldv + hk * D;
 
-  LaneOff<D> lo;
+  LaneOff<T, D> lo;
   lo.init(lane);
-  bf16x8 qf[NKS];  // B operand of S^T = K Q^T: lane holds Q[qw + l32][16 ks + 8 h2 .. +7]
+  V8<T> qf[NKS];  // B operand of S^T = K Q^T: lane holds Q[qw + l32][16 ks + 8 h2 .. +7]
   const int qrow = qw + l32;
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks)
-    qf[ks] = qrow < S ? *reinterpret_cast<const bf16x8*>(Qb + (long)qrow * ldq + 16 * ks + 8 * h2) : bf16x8{};
+    qf[ks] = qrow < S ? *reinterpret_cast<const V8<T>*>(Qb + (long)qrow * ldq + 16 * ks + 8 * h2) : V8<T>{};
 
   f32x16 o[NDB];
 #pragma unroll
@@ -249,7 +264,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_kernel(const __bf16* __restric
   const int kend = CAUSAL ? min(S, q0 + QT) : S;
   const int nkt = (kend + KT - 1) / KT;
 
-  Stage<D, KT, NW * 64> sk, sv;
+  Stage<T, D, KT, NW * 64> sk, sv;
   sk.load(Kb, ldk, 0, S);
   sv.load(Vb, ldv, 0, S);
   sk.store(smem);
@@ -260,8 +275,8 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_kernel(const __bf16* __restric
 
   auto body = [&](auto cc, int kt) {
     constexpr int CUR = decltype(cc)::value;
-    const __bf16* Kt = smem + 2 * CUR * TILE;
-    const __bf16* Vt = Kt + TILE;
+    const T* Kt = smem + 2 * CUR * TILE;
+    const T* Vt = Kt + TILE;
     const int k0 = kt * KT;
     const bool more = kt + 1 < nkt;
     if (more) {  // issue-early / write-late staging of the next K/V tile (T14)
@@ -271,10 +286,10 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_kernel(const __bf16* __restric
     if (!(CAUSAL && k0 > qw + 31)) {
       // S^T = K Q^T, two 32-key halves, next fragments issued before the current MFMAs
       f32x16 s0 = f32x16{}, s1 = f32x16{};
-      bf16x8 a0 = lo.rowk(Kt, 0, 0), a1 = lo.rowk(Kt, 32, 0);
+      V8<T> a0 = lo.rowk(Kt, 0, 0), a1 = lo.rowk(Kt, 32, 0);
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
-        bf16x8 n0 = a0, n1 = a1;
+        V8<T> n0 = a0, n1 = a1;
         if (ks + 1 < NKS) {
           n0 = lo.rowk(Kt, 0, ks + 1);
           n1 = lo.rowk(Kt, 32, ks + 1);
@@ -289,6 +304,13 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_kernel(const __bf16* __restric
         for (int r = 0; r < 16; ++r) {
           if (k0 + crow(r, h2) > qrow) s0[r] = -INFINITY;
           if (k0 + 32 + crow(r, h2) > qrow) s1[r] = -INFINITY;
+        }
+      }
+      if (!CAUSAL && k0 + KT > skv) {  // zero-padded sequence: keys >= skv do not exist
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          if (k0 + crow(r, h2) >= skv) s0[r] = -INFINITY;
+          if (k0 + 32 + crow(r, h2) >= skv) s1[r] = -INFINITY;
         }
       }
       float mx = -INFINITY;
@@ -312,15 +334,15 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_kernel(const __bf16* __restric
         rs += s0[r] + s1[r];
       }
       l_i += half_sum(rs);
-      const bf16x8 p00 = pack8(s0, 0), p01 = pack8(s0, 1), p10 = pack8(s1, 0), p11 = pack8(s1, 1);
+      const V8<T> p00 = pack8<T>(s0, 0), p01 = pack8<T>(s0, 1), p10 = pack8<T>(s1, 0), p11 = pack8<T>(s1, 1);
       // O^T[d][q] += V^T[d][key] P^T[key][q]; V^T fragments prefetched one MFMA ahead
-      bf16x8 vc = lo.tr(Vt, 0, 0);
+      V8<T> vc = lo.tr(Vt, 0, 0);
 #pragma unroll
       for (int st = 0; st < 4 * NDB; ++st) {
         const int k4 = st / NDB, db = st % NDB;
-        bf16x8 vn = vc;
+        V8<T> vn = vc;
         if (st + 1 < 4 * NDB) vn = lo.tr(Vt, ((st + 1) / NDB) * 16, (st + 1) % NDB);
-        const bf16x8 pf = k4 == 0 ? p00 : k4 == 1 ? p01 : k4 == 2 ? p10 : p11;
+        const V8<T> pf = k4 == 0 ? p00 : k4 == 1 ? p01 : k4 == 2 ? p10 : p11;
         o[db] = mfma(vc, pf, o[db]);
         vc = vn;
       }
@@ -338,7 +360,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_kernel(const __bf16* __restric
 
   {
     const float inv = 1.f / l_i;
-    store_rows16<NDB>(o, inv, O + ((long)b * S + qrow) * ldo + hq * D, qrow < S, h2);
+    store_rows16<T, NDB>(o, inv, O + ((long)b * S + qrow) * ldo + hq * D, qrow < S, h2);
     if (qrow < S && h2 == 0) LSE[((long)b * Hq + hq) * S + qrow] = (m_i + __log2f(l_i)) * 0.69314718055994531f;
   }
 }
@@ -354,14 +376,14 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_kernel(const __bf16* __restric
 // iteration t and written into the slot tile t-1 vacated, one barrier per tile. In causal mode a
 // wave's only diagonal tile is its last one.
 // ======================================================================================
-template <int D, bool CAUSAL, int NW>
-__global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const __bf16* __restrict__ Q, const __bf16* __restrict__ K,
-                                                           const __bf16* __restrict__ V, __bf16* __restrict__ O,
+template <typename T, int D, bool CAUSAL, int NW>
+__global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const T* __restrict__ Q, const T* __restrict__ K,
+                                                           const T* __restrict__ V, T* __restrict__ O,
                                                            float* __restrict__ LSE, int S, int Hq, int Hkv, long ldq,
                                                            long ldk, long ldv, long ldo, float scale_log2) {
   constexpr int KT = 64, QT = 32 * NW;
   constexpr int NKS = D / 16, NDB = D / 32, TILE = KT * D;
-  __shared__ __attribute__((aligned(16))) __bf16 smem[6 * TILE];  // (K V) x 3
+  __shared__ __attribute__((aligned(16))) T smem[6 * TILE];  // (K V) x 3
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h2 = lane >> 5, l32 = lane & 31;
   const int nqt = (S + QT - 1) / QT;
@@ -372,17 +394,17 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const __bf16* __restr
   const int hk = hq / (Hq / Hkv);
   const int q0 = qt * QT, qw = q0 + wid * 32;
 
-  const __bf16* Qb = Q + (long)b * S * ldq + hq * D;
-  const __bf16* Kb = K + (long)b * S * ldk + hk * D;
-  const __bf16* Vb = V + (long)b * S * ldv + hk * D;
+  const T* Qb = Q + (long)b * S * ldq + hq * D;
+  const T* Kb = K + (long)b * S * ldk + hk * D;
+  const T* Vb = V + (long)b * S * ldv + hk * D;
 
-  LaneOff<D> lo;
+  LaneOff<T, D> lo;
   lo.init(lane);
-  bf16x8 qf[NKS];
+  V8<T> qf[NKS];
   const int qrow = qw + l32;
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks)
-    qf[ks] = qrow < S ? *reinterpret_cast<const bf16x8*>(Qb + (long)qrow * ldq + 16 * ks + 8 * h2) : bf16x8{};
+    qf[ks] = qrow < S ? *reinterpret_cast<const V8<T>*>(Qb + (long)qrow * ldq + 16 * ks + 8 * h2) : V8<T>{};
 
   f32x16 o[NDB];
 #pragma unroll
@@ -393,7 +415,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const __bf16* __restr
   const int nkt = (kend + KT - 1) / KT;
   const int lastw = CAUSAL ? min(nkt - 1, (qw + 31) / KT) : nkt - 1;  // this wave's last tile
 
-  GStage<D, KT, NW> gk, gv;  // LDS-DMA (S % 64 == 0: tiles are always full)
+  GStage<T, D, KT, NW> gk, gv;  // LDS-DMA (S % 64 == 0: tiles are always full)
   gk.init(ldk);
   gv.init(ldv);
   auto slot = [&](int t) { return smem + 2 * (t % 3) * TILE; };
@@ -423,7 +445,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const __bf16* __restr
 
   f32x16 c0 = f32x16{}, c1 = f32x16{};  // scores of the tile being finished (two 32-key halves)
   if (lastw >= 0) {
-    const __bf16* Kt = slot(0);
+    const T* Kt = slot(0);
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
       c0 = mfma(lo.rowk(Kt, 0, ks), qf[ks], c0);
@@ -437,16 +459,16 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const __bf16* __restr
   // address is a lane-constant base plus an immediate offset
   auto body = [&](auto cur_c, int t) {
     constexpr int CUR = decltype(cur_c)::value;
-    __bf16* const s_cur = smem + 2 * CUR * TILE;
-    __bf16* const s_nxt = smem + 2 * ((CUR + 1) % 3) * TILE;
-    __bf16* const s_nn = smem + 2 * ((CUR + 2) % 3) * TILE;
+    T* const s_cur = smem + 2 * CUR * TILE;
+    T* const s_nxt = smem + 2 * ((CUR + 1) % 3) * TILE;
+    T* const s_nn = smem + 2 * ((CUR + 2) % 3) * TILE;
     if (t + 2 < nkt) {  // LDS-DMA of tile t + 2 into the slot tile t - 1 vacated
       gk.issue(Kb + (long)(t + 2) * KT * ldk, s_nn);
       gv.issue(Vb + (long)(t + 2) * KT * ldv, s_nn + TILE);
     }
     if (t <= lastw) {
-      const __bf16* Kn = s_nxt;
-      const __bf16* Vt = s_cur + TILE;
+      const T* Kn = s_nxt;
+      const T* Vt = s_cur + TILE;
       auto iter = [&](auto next_c, auto diag_c) {
         constexpr bool NEXT = decltype(next_c)::value, DIAG = decltype(diag_c)::value;
         constexpr int RA = NKS, EA = 32 / RA;  // phase A: regions / softmax elements per region
@@ -463,10 +485,10 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const __bf16* __restr
           }
         };
         // phase A: S(t+1) | exp, row sum of tile t
-        bf16x8 a0 = lo.rowk(Kn, 0, 0), a1 = lo.rowk(Kn, 32, 0);
+        V8<T> a0 = lo.rowk(Kn, 0, 0), a1 = lo.rowk(Kn, 32, 0);
 #pragma unroll
         for (int k = 0; k < RA; ++k) {
-          bf16x8 b0 = a0, b1 = a1;
+          V8<T> b0 = a0, b1 = a1;
           if (NEXT && k + 1 < RA) {
             b0 = lo.rowk(Kn, 0, k + 1);
             b1 = lo.rowk(Kn, 32, k + 1);
@@ -482,13 +504,13 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const __bf16* __restr
           __builtin_amdgcn_sched_barrier(0);
         }
         l_i += half_sum(rs);
-        const bf16x8 p[4] = {pack8(c0, 0), pack8(c0, 1), pack8(c1, 0), pack8(c1, 1)};
+        const V8<T> p[4] = {pack8<T>(c0, 0), pack8<T>(c0, 1), pack8<T>(c1, 0), pack8<T>(c1, 1)};
         if (NEXT && DIAG) mask(n0, n1, (t + 1) * KT);
         // phase B: O^T += V_t^T P_t | row max of tile t+1
-        bf16x8 vc[2] = {lo.tr(Vt, 0, 0), lo.tr(Vt, (1 / NDB) * 16, 1 % NDB)};
+        V8<T> vc[2] = {lo.tr(Vt, 0, 0), lo.tr(Vt, (1 / NDB) * 16, 1 % NDB)};
 #pragma unroll
         for (int k = 0; k < RB; ++k) {
-          bf16x8 vn[2] = {vc[0], vc[1]};
+          V8<T> vn[2] = {vc[0], vc[1]};
           if (k + 1 < RB) {
             const int s0 = 2 * (k + 1), s1 = s0 + 1;
             vn[0] = lo.tr(Vt, (s0 / NDB) * 16, s0 % NDB);
@@ -536,7 +558,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const __bf16* __restr
 
   {
     const float inv = 1.f / l_i;
-    store_rows16<NDB>(o, inv, O + ((long)b * S + qrow) * ldo + hq * D, qrow < S, h2);
+    store_rows16<T, NDB>(o, inv, O + ((long)b * S + qrow) * ldo + hq * D, qrow < S, h2);
     if (qrow < S && h2 == 0) LSE[((long)b * Hq + hq) * S + qrow] = (m_i + __log2f(l_i)) * 0.69314718055994531f;
   }
 }
@@ -550,8 +572,8 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const __bf16* __restr
 // ======================================================================================
 constexpr int PRE_QB = 16;
 constexpr int PRE_MAXH = 128;
-template <int D>
-__global__ __launch_bounds__(256) void bwd_pre_kernel(const __bf16* __restrict__ O, const __bf16* __restrict__ dO,
+template <typename T, int D>
+__global__ __launch_bounds__(256) void bwd_pre_kernel(const T* __restrict__ O, const T* __restrict__ dO,
                                                       float* __restrict__ delta, int B, int S, int Hq, long ldo,
                                                       long lddo) {
   constexpr int LPR = D / 8;     // lanes per row
@@ -571,8 +593,8 @@ __global__ __launch_bounds__(256) void bwd_pre_kernel(const __bf16* __restrict__
       if (r < rows) {
         const long t = tok0 + r / Hq;
         const int h = r % Hq;
-        load8<__bf16>(O + t * ldo + h * D + sub * 8, a[u]);
-        load8<__bf16>(dO + t * lddo + h * D + sub * 8, c[u]);
+        load8<T>(O + t * ldo + h * D + sub * 8, a[u]);
+        load8<T>(dO + t * lddo + h * D + sub * 8, c[u]);
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) a[u][j] = c[u][j] = 0.f;
@@ -609,23 +631,23 @@ __global__ __launch_bounds__(256) void bwd_pre_kernel(const __bf16* __restrict__
 // NW = 4 (128 keys, 80 KB, two blocks per CU): the constants arrive as one float per lane and are
 // broadcast with ds_bpermute (no LDS left for them).
 // ======================================================================================
-template <int D, bool CAUSAL, int NW>
+template <typename T, int D, bool CAUSAL, int NW>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
-    const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ V,
-    const __bf16* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
-    __bf16* __restrict__ dK, __bf16* __restrict__ dV, int S, int Hq, int Hkv, long ldq, long ldk, long ldv,
-    long lddo, long lddk, long lddv, float scale, float scale_log2, int prio) {
+    const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V,
+    const T* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
+    T* __restrict__ dK, T* __restrict__ dV, int S, int Hq, int Hkv, long ldq, long ldk, long ldv,
+    long lddo, long lddk, long lddv, float scale, float scale_log2, int prio, int skv) {
   constexpr int KB = 32 * NW, QT = 32, NT = NW * 64;
   constexpr int NKS = D / 16, NDB = D / 32;
   constexpr int KVT = KB * D, QDT = QT * D;
   constexpr bool ROWC_LDS = NW == 8;
   // Q and dO first: their (transposed) reads then use 16-bit immediate offsets off one base
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * KVT + 2 * QDT];  // Q dO K V
+  __shared__ __attribute__((aligned(16))) T smem[2 * KVT + 2 * QDT];  // Q dO K V
   __shared__ __attribute__((aligned(16))) float rowc[ROWC_LDS ? 2 : 1][32];  // lse*log2e | delta
-  __bf16* const Qs = smem;
-  __bf16* const Ds = smem + QDT;
-  __bf16* const Ks = smem + 2 * QDT;
-  __bf16* const Vs = smem + 2 * QDT + KVT;
+  T* const Qs = smem;
+  T* const Ds = smem + QDT;
+  T* const Ks = smem + 2 * QDT;
+  T* const Vs = smem + 2 * QDT + KVT;
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h2 = lane >> 5, l32 = lane & 31;
   const int nkb = S / KB;
@@ -638,15 +660,15 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
   const int krow = kw + l32;
 
   {
-    GStage<D, KB, NW> gk, gv;
+    GStage<T, D, KB, NW> gk, gv;
     gk.init(ldk);
     gv.init(ldv);
     gk.issue(K + ((long)b * S + k0) * ldk + hk * D, Ks);
     gv.issue(V + ((long)b * S + k0) * ldv + hk * D, Vs);
   }
-  const __bf16* Kw = Ks + wid * 32 * D;
-  const __bf16* Vw = Vs + wid * 32 * D;
-  LaneOff<D> lo;
+  const T* Kw = Ks + wid * 32 * D;
+  const T* Vw = Vs + wid * 32 * D;
+  LaneOff<T, D> lo;
   lo.init(lane);
 
   f32x16 dkt[NDB], dvt[NDB];
@@ -662,7 +684,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
   int bp_base = 4 * (4 * h2);  // ds_bpermute byte address of lane crow(0, h2)
   asm volatile("" : "+v"(bp_base));  // opaque: per-row offsets then fold into the ds offset field
 
-  Stage<D, QT, NT> sq, sd;
+  Stage<T, D, QT, NT> sq, sd;
   float rc_next = 0.f;
   auto stage_load = [&](int it) {
     const int hq = hk * nrep + it / nqt;
@@ -692,11 +714,11 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
     if (!(CAUSAL && q0 + QT - 1 < kw)) {
       f32x16 s = f32x16{}, dp = f32x16{};
       // S chain then dP chain: one operand pair in flight ahead of each MFMA
-      bf16x8 xa = lo.rowk(Qs, 0, 0), xb = lo.rowk(Kw, 0, 0);
+      V8<T> xa = lo.rowk(Qs, 0, 0), xb = lo.rowk(Kw, 0, 0);
 #pragma unroll
       for (int st = 0; st < 2 * NKS; ++st) {
         const int ks = st % NKS;
-        bf16x8 na = xa, nb = xb;
+        V8<T> na = xa, nb = xb;
         if (st + 1 < 2 * NKS) {
           const int nks = (st + 1) % NKS;
           na = lo.rowk(st + 1 < NKS ? Qs : Ds, 0, nks);
@@ -728,16 +750,17 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
           const int r = 4 * rr + j;
           float p = fexp2(fmaf(s[r], scale_log2, -lse4[j]));
           if (diag && l32 > crow(r, h2)) p = 0.f;
+          if (!CAUSAL && krow >= skv) p = 0.f;  // padded key
           s[r] = p;
           dp[r] = p * (dp[r] - dl4[j]);
         }
       }
-      const bf16x8 p0 = pack8(s, 0), p1 = pack8(s, 1), d0 = pack8(dp, 0), d1 = pack8(dp, 1);
-      bf16x8 ot = lo.tr(Ds, 0, 0), qt = lo.tr(Qs, 0, 0);
+      const V8<T> p0 = pack8<T>(s, 0), p1 = pack8<T>(s, 1), d0 = pack8<T>(dp, 0), d1 = pack8<T>(dp, 1);
+      V8<T> ot = lo.tr(Ds, 0, 0), qt = lo.tr(Qs, 0, 0);
 #pragma unroll
       for (int st = 0; st < 2 * NDB; ++st) {
         const int s2 = st / NDB, db = st % NDB;
-        bf16x8 no = ot, nq = qt;
+        V8<T> no = ot, nq = qt;
         if (st + 1 < 2 * NDB) {
           no = lo.tr(Ds, 16 * ((st + 1) / NDB), (st + 1) % NDB);
           nq = lo.tr(Qs, 16 * ((st + 1) / NDB), (st + 1) % NDB);
@@ -750,8 +773,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
     __syncthreads();
   }
 
-  store_rows16<NDB>(dkt, scale, dK + ((long)b * S + krow) * lddk + hk * D, true, h2);
-  store_rows16<NDB>(dvt, 1.f, dV + ((long)b * S + krow) * lddv + hk * D, true, h2);
+  store_rows16<T, NDB>(dkt, scale, dK + ((long)b * S + krow) * lddk + hk * D, true, h2);
+  store_rows16<T, NDB>(dvt, 1.f, dV + ((long)b * S + krow) * lddv + hk * D, true, h2);
 }
 
 // ======================================================================================
@@ -765,20 +788,20 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
 // K/V of the block stay in LDS (64 KB at D = 128). Q/dO steps (32 KB) and their per-query
 // constants (lse*log2e, delta) arrive by LDS-DMA into a double buffer, issued one step ahead.
 // ======================================================================================
-template <int D, bool CAUSAL>
+template <typename T, int D, bool CAUSAL>
 __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
-    const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ V,
-    const __bf16* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
-    __bf16* __restrict__ dK, __bf16* __restrict__ dV, int S, int Hq, int Hkv, long ldq, long ldk, long ldv,
-    long lddo, long lddk, long lddv, float scale, float scale_log2) {
+    const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V,
+    const T* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
+    T* __restrict__ dK, T* __restrict__ dV, int S, int Hq, int Hkv, long ldq, long ldk, long ldv,
+    long lddo, long lddk, long lddv, float scale, float scale_log2, int skv) {
   constexpr int NW = 4, KB = 32 * NW, QS = 64;
   constexpr int NKS = D / 16, NDB = D / 32;
   constexpr int KVT = KB * D, QDT = QS * D;
   // Q0 dO0 Q1 dO1 (steps, double-buffered) | K V | row constants [buf][lse, delta][64]
-  __shared__ __attribute__((aligned(16))) __bf16 smem[4 * QDT + 2 * KVT];
+  __shared__ __attribute__((aligned(16))) T smem[4 * QDT + 2 * KVT];
   __shared__ __attribute__((aligned(16))) float rowc[2][2][QS];
-  __bf16* const Ks = smem + 4 * QDT;
-  __bf16* const Vs = Ks + KVT;
+  T* const Ks = smem + 4 * QDT;
+  T* const Vs = Ks + KVT;
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h2 = lane >> 5, l32 = lane & 31;
   const int nkb = S / KB;
@@ -789,7 +812,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
   const int nrep = Hq / Hkv;
   const int k0 = kbk * KB, kw = k0 + wid * 32;
 
-  GStage<D, QS, NW> gq, gd;
+  GStage<T, D, QS, NW> gq, gd;
   gq.init(ldq);
   gd.init(lddo);
   const int qstart = CAUSAL ? k0 : 0;
@@ -807,16 +830,16 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
     }
   };
   {
-    GStage<D, KB, NW> gk, gv;
+    GStage<T, D, KB, NW> gk, gv;
     gk.init(ldk);
     gv.init(ldv);
     gk.issue(K + ((long)b * S + k0) * ldk + hk * D, Ks);
     gv.issue(V + ((long)b * S + k0) * ldv + hk * D, Vs);
   }
   if (total > 0) issue_step(0, 0);
-  const __bf16* Kw = Ks + wid * 32 * D;
-  const __bf16* Vw = Vs + wid * 32 * D;
-  LaneOff<D> lo;
+  const T* Kw = Ks + wid * 32 * D;
+  const T* Vw = Vs + wid * 32 * D;
+  LaneOff<T, D> lo;
   lo.init(lane);
 
   f32x16 dkt[NDB], dvt[NDB];
@@ -828,8 +851,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
     const int cur = it & 1;
     const int q0 = qstart + (it % nqs) * QS;
     if (it + 1 < total) issue_step(it + 1, 1 - cur);  // lands under this step's MFMAs
-    const __bf16* Qs = smem + cur * 2 * QDT;
-    const __bf16* Ds = Qs + QDT;
+    const T* Qs = smem + cur * 2 * QDT;
+    const T* Ds = Qs + QDT;
     const float* lrow = &rowc[cur][0][0];
     const float* drow = &rowc[cur][1][0];
 
@@ -848,9 +871,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
       constexpr int EA = 16 / R1, EB = 16 / R3;  // softmax rows per region
       const int lim = kw + l32 - q0 - 4 * h2;
       f32x16 sa = f32x16{}, sb = f32x16{}, pa = f32x16{}, pb = f32x16{};
-      bf16x8 pA[2], gA[2], pB[2], gB[2];
+      V8<T> pA[2], gA[2], pB[2], gB[2];
       f32x4 lc[4], dc[4];  // row constants of the sub-tile being softmaxed
-      auto fetch = [&](int k, bf16x8 (&o)[4]) {
+      auto fetch = [&](int k, V8<T> (&o)[4]) {
         if (k < 2 * R1) {
           const int ks = k % R1, r0 = 32 * (k / R1);
           o[0] = lo.rowk(Qs, r0, ks);
@@ -873,10 +896,11 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
       auto soft = [&](f32x16& sv, f32x16& dp, int u, int r) {
         float p = fexp2(fmaf(sv[r], scale_log2, -lc[r >> 2][r & 3] * 1.4426950408889634f));
         if (MASK && crow(r, 0) < lim - 32 * u) p = 0.f;
+        if (!CAUSAL && kw + l32 >= skv) p = 0.f;  // padded key
         sv[r] = p;
         dp[r] = p * (dp[r] - dc[r >> 2][r & 3]);
       };
-      bf16x8 cur[4], nxt[4];
+      V8<T> cur[4], nxt[4];
       fetch(0, cur);
       load_rc(0);
 #pragma unroll
@@ -891,7 +915,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
 #pragma unroll
           for (int e = 0; e < EA; ++e) soft(sa, pa, 0, (k - R1) * EA + e);
           if (k == 2 * R1 - 1) {
-            pA[0] = pack8(sa, 0); pA[1] = pack8(sa, 1); gA[0] = pack8(pa, 0); gA[1] = pack8(pa, 1);
+            pA[0] = pack8<T>(sa, 0); pA[1] = pack8<T>(sa, 1); gA[0] = pack8<T>(pa, 0); gA[1] = pack8<T>(pa, 1);
             load_rc(1);
           }
         } else {
@@ -903,7 +927,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
 #pragma unroll
             for (int e = 0; e < EB; ++e) soft(sb, pb, 1, j * EB + e);
             if (j == R3 - 1) {
-              pB[0] = pack8(sb, 0); pB[1] = pack8(sb, 1); gB[0] = pack8(pb, 0); gB[1] = pack8(pb, 1);
+              pB[0] = pack8<T>(sb, 0); pB[1] = pack8<T>(sb, 1); gB[0] = pack8<T>(pb, 0); gB[1] = pack8<T>(pb, 1);
             }
           }
         }
@@ -919,8 +943,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
   }
 
   const int krow = kw + l32;
-  store_rows16<NDB>(dkt, scale, dK + ((long)b * S + krow) * lddk + hk * D, true, h2);
-  store_rows16<NDB>(dvt, 1.f, dV + ((long)b * S + krow) * lddv + hk * D, true, h2);
+  store_rows16<T, NDB>(dkt, scale, dK + ((long)b * S + krow) * lddk + hk * D, true, h2);
+  store_rows16<T, NDB>(dvt, 1.f, dV + ((long)b * S + krow) * lddv + hk * D, true, h2);
 }
 
 // ======================================================================================
@@ -932,15 +956,15 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
 // PIPE: the same tile work as explicit sched_barrier regions -- S/dP of the second 32-key half
 // interleaved with the softmax of the first, dQ of the first with the softmax of the second (see
 // bwd_dkdv_p2_kernel) -- instead of two back-to-back MFMA -> VALU -> MFMA halves.
-template <int D, bool CAUSAL, int NW, bool PIPE = false>
+template <typename T, int D, bool CAUSAL, int NW, bool PIPE = false>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
-    const __bf16* __restrict__ Q, const __bf16* __restrict__ K, const __bf16* __restrict__ V,
-    const __bf16* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
-    __bf16* __restrict__ dQ, int S, int Hq, int Hkv, long ldq, long ldk, long ldv, long lddo, long lddq,
-    float scale, float scale_log2, int prio) {
+    const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V,
+    const T* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
+    T* __restrict__ dQ, int S, int Hq, int Hkv, long ldq, long ldk, long ldv, long lddo, long lddq,
+    float scale, float scale_log2, int prio, int skv) {
   constexpr int KT = 64, QT = 32 * NW;
   constexpr int NKS = D / 16, NDB = D / 32, TILE = KT * D;
-  __shared__ __attribute__((aligned(16))) __bf16 smem[4 * TILE];  // K0 V0 K1 V1
+  __shared__ __attribute__((aligned(16))) T smem[4 * TILE];  // K0 V0 K1 V1
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h2 = lane >> 5, l32 = lane & 31;
   const int nqt = (S + QT - 1) / QT;
@@ -952,23 +976,23 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
   const int q0 = qt * QT, qw = q0 + wid * 32;
   const int qrow = qw + l32;
 
-  const __bf16* Kb = K + (long)b * S * ldk + hk * D;
-  const __bf16* Vb = V + (long)b * S * ldv + hk * D;
+  const T* Kb = K + (long)b * S * ldk + hk * D;
+  const T* Vb = V + (long)b * S * ldv + hk * D;
 
-  LaneOff<D> lo;
+  LaneOff<T, D> lo;
   lo.init(lane);
-  bf16x8 qf[NKS], df[NKS];
+  V8<T> qf[NKS], df[NKS];
   {
-    const __bf16* Qr = Q + ((long)b * S + qrow) * ldq + hq * D + 8 * h2;
-    const __bf16* Dr = dO + ((long)b * S + qrow) * lddo + hq * D + 8 * h2;
+    const T* Qr = Q + ((long)b * S + qrow) * ldq + hq * D + 8 * h2;
+    const T* Dr = dO + ((long)b * S + qrow) * lddo + hq * D + 8 * h2;
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
       if (qrow < S) {
-        qf[ks] = *reinterpret_cast<const bf16x8*>(Qr + 16 * ks);
-        df[ks] = *reinterpret_cast<const bf16x8*>(Dr + 16 * ks);
+        qf[ks] = *reinterpret_cast<const V8<T>*>(Qr + 16 * ks);
+        df[ks] = *reinterpret_cast<const V8<T>*>(Dr + 16 * ks);
       } else {
-        qf[ks] = bf16x8{};
-        df[ks] = bf16x8{};
+        qf[ks] = V8<T>{};
+        df[ks] = V8<T>{};
       }
     }
   }
@@ -985,7 +1009,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
   const int kend = CAUSAL ? min(S, q0 + QT) : S;
   const int nkt = (kend + KT - 1) / KT;
 
-  GStage<D, KT, NW> gk, gv;
+  GStage<T, D, KT, NW> gk, gv;
   gk.init(ldk);
   gv.init(ldv);
   gk.issue(Kb, smem);
@@ -995,8 +1019,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
 
   auto body = [&](auto cc, int kt) {
     constexpr int CUR = decltype(cc)::value;
-    const __bf16* Kt = smem + 2 * CUR * TILE;
-    const __bf16* Vt = Kt + TILE;
+    const T* Kt = smem + 2 * CUR * TILE;
+    const T* Vt = Kt + TILE;
     const int k0 = kt * KT;
     if (kt + 1 < nkt) {  // LDS-DMA of the next tile runs under this tile's MFMAs
       gk.issue(Kb + (long)(k0 + KT) * ldk, smem + 2 * (1 - CUR) * TILE);
@@ -1010,8 +1034,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
         constexpr int EA = 16 / R1, EB = 16 / R3;
         const int lim = qrow - k0 - 4 * h2;
         f32x16 s0 = f32x16{}, s1 = f32x16{}, p0 = f32x16{}, p1 = f32x16{};
-        bf16x8 g0[2], g1[2];
-        auto fetch = [&](int k, bf16x8 (&o)[4]) {
+        V8<T> g0[2], g1[2];
+        auto fetch = [&](int k, V8<T> (&o)[4]) {
           if (k < 2 * R1) {
             const int ks = k % R1, r0 = 32 * (k / R1);
             o[0] = lo.rowk(Kt, r0, ks);
@@ -1028,7 +1052,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
           if (MASK && crow(r, 0) > lim - 32 * kb) p = 0.f;
           dp[r] = p * (dp[r] - dl);
         };
-        bf16x8 cur[4], nxt[4];
+        V8<T> cur[4], nxt[4];
         fetch(0, cur);
 #pragma unroll
         for (int k = 0; k < NR; ++k) {
@@ -1043,7 +1067,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
               p1 = mfma(cur[1], df[ks], p1);
 #pragma unroll
               for (int e = 0; e < EA; ++e) soft(s0, p0, 0, (k - R1) * EA + e);
-              if (k == 2 * R1 - 1) { g0[0] = pack8(p0, 0); g0[1] = pack8(p0, 1); }
+              if (k == 2 * R1 - 1) { g0[0] = pack8<T>(p0, 0); g0[1] = pack8<T>(p0, 1); }
             }
           } else {
             const int jj = k - 2 * R1, j = jj % R3;
@@ -1054,7 +1078,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
             if (!second) {
 #pragma unroll
               for (int e = 0; e < EB; ++e) soft(s1, p1, 1, j * EB + e);
-              if (j == R3 - 1) { g1[0] = pack8(p1, 0); g1[1] = pack8(p1, 1); }
+              if (j == R3 - 1) { g1[0] = pack8<T>(p1, 0); g1[1] = pack8<T>(p1, 1); }
             }
           }
 #pragma unroll
@@ -1062,7 +1086,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
           __builtin_amdgcn_sched_barrier(0);
         }
       };
-      if (!CAUSAL || k0 + KT - 1 <= qw) tile(std::false_type{});
+      if (!CAUSAL || k0 + KT - 1 <= qw) tile(std::false_type{});  // (non-causal + padded keys: PIPE off)
       else if (k0 <= qw + 31) tile(std::true_type{});  // diagonal tile (else fully masked)
     } else {
 #pragma unroll
@@ -1070,10 +1094,10 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
       const int kh = k0 + 32 * kb;
       if (CAUSAL && kh > qw + 31) continue;  // wave-uniform: this key half is fully masked
       f32x16 s = f32x16{}, dp = f32x16{};
-      bf16x8 ka = lo.rowk(Kt, 32 * kb, 0), va = lo.rowk(Vt, 32 * kb, 0);
+      V8<T> ka = lo.rowk(Kt, 32 * kb, 0), va = lo.rowk(Vt, 32 * kb, 0);
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
-        bf16x8 nk = ka, nv = va;
+        V8<T> nk = ka, nv = va;
         if (ks + 1 < NKS) {
           nk = lo.rowk(Kt, 32 * kb, ks + 1);
           nv = lo.rowk(Vt, 32 * kb, ks + 1);
@@ -1087,14 +1111,15 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
       for (int r = 0; r < 16; ++r) {
         float p = fexp2(fmaf(s[r], scale_log2, -lse2));
         if (diag && kh + crow(r, h2) > qrow) p = 0.f;
+        if (!CAUSAL && kh + crow(r, h2) >= skv) p = 0.f;  // padded key
         dp[r] = p * (dp[r] - dl);
       }
-      const bf16x8 d0 = pack8(dp, 0), d1 = pack8(dp, 1);
-      bf16x8 kc = lo.tr(Kt, 32 * kb, 0);
+      const V8<T> d0 = pack8<T>(dp, 0), d1 = pack8<T>(dp, 1);
+      V8<T> kc = lo.tr(Kt, 32 * kb, 0);
 #pragma unroll
       for (int st = 0; st < 2 * NDB; ++st) {
         const int s2 = st / NDB, db = st % NDB;
-        bf16x8 kn = kc;
+        V8<T> kn = kc;
         if (st + 1 < 2 * NDB) kn = lo.tr(Kt, 32 * kb + 16 * ((st + 1) / NDB), (st + 1) % NDB);
         dqt[db] = mfma(kc, s2 ? d1 : d0, dqt[db]);
         kc = kn;
@@ -1108,7 +1133,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
     if (kt + 1 < nkt) body(IC<1>{}, kt + 1);
   }
 
-  store_rows16<NDB>(dqt, scale, dQ + ((long)b * S + qrow) * lddq + hq * D, qrow < S, h2);
+  store_rows16<T, NDB>(dqt, scale, dQ + ((long)b * S + qrow) * lddq + hq * D, qrow < S, h2);
 }
 
 }  // namespace attn
@@ -1116,11 +1141,12 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
 
 using namespace pra::attn;
 
-extern "C" {
+namespace {
 
-// All tensors bf16, layout [B, S, H, D] with token stride ld* (elements); LSE/Delta fp32 [B, Hq, S].
-hipError_t pra_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int Hq,
-                        int Hkv, int D, long ldq, long ldk, long ldv, long ldo, float scale, int causal,
+// All tensors bf16 or fp16 (T), layout [B, S, H, D] with token stride ld* (elements); LSE/Delta fp32 [B, Hq, S].
+template <typename T>
+hipError_t attn_fwd_t(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int Hq,
+                        int Hkv, int D, long ldq, long ldk, long ldv, long ldo, float scale, int causal, int skv,
                         hipStream_t st) {
   if (S % 64 || (D != 64 && D != 128) || Hq % Hkv) return hipErrorInvalidValue;
   if (ldq % 8 || ldk % 8 || ldv % 8 || ldo % 8) return hipErrorInvalidValue;
@@ -1132,24 +1158,26 @@ hipError_t pra_attn_fwd(const void* q, const void* k, const void* v, void* o, fl
   // attention (B8 S2048 H32: 0.460 -> 0.422 ms; S8192 H32/8: 0.654 -> 0.615 ms). Its non-causal
   // instantiation spills at D = 128, so full attention stays on fwd_kernel.
   const char* fp = getenv("PRA_FWD_PIPE");
-  const bool pipe = fp ? atoi(fp) != 0 : (causal != 0);
+  // non-causal with padded keys (skv < S) needs fwd_kernel's key bound
+  const bool pipe = (causal || skv >= S) && (fp ? atoi(fp) != 0 : (causal != 0));
 #define LAUNCH(DD, CC)                                                                                        \
   if (pipe)                                                                                                   \
-    hipLaunchKernelGGL((fwd_p_kernel<DD, CC, NW>), grid, block, 0, st, (const __bf16*)q, (const __bf16*)k,         \
-                       (const __bf16*)v, (__bf16*)o, lse, S, Hq, Hkv, ldq, ldk, ldv, ldo, sl2);                  \
+    hipLaunchKernelGGL((fwd_p_kernel<T, DD, CC, NW>), grid, block, 0, st, (const T*)q, (const T*)k,         \
+                       (const T*)v, (T*)o, lse, S, Hq, Hkv, ldq, ldk, ldv, ldo, sl2);                  \
   else                                                                                                        \
-  hipLaunchKernelGGL((fwd_kernel<DD, CC, NW>), grid, block, 0, st, (const __bf16*)q, (const __bf16*)k,             \
-                     (const __bf16*)v, (__bf16*)o, lse, S, Hq, Hkv, ldq, ldk, ldv, ldo, sl2)
+  hipLaunchKernelGGL((fwd_kernel<T, DD, CC, NW>), grid, block, 0, st, (const T*)q, (const T*)k,             \
+                     (const T*)v, (T*)o, lse, S, Hq, Hkv, ldq, ldk, ldv, ldo, sl2, skv)
   if (D == 128) { if (causal) LAUNCH(128, true); else LAUNCH(128, false); }
   else { if (causal) LAUNCH(64, true); else LAUNCH(64, false); }
 #undef LAUNCH
   return hipGetLastError();
 }
 
-hipError_t pra_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
+template <typename T>
+hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o, const void* dout,
                         const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int S, int Hq, int Hkv,
                         int D, long ldq, long ldk, long ldv, long ldo, long lddo, long lddq, long lddk, long lddv,
-                        float scale, int causal, hipStream_t st) {
+                        float scale, int causal, int skv, hipStream_t st) {
   if (S % 128 || (D != 64 && D != 128) || Hq % Hkv) return hipErrorInvalidValue;
   if (ldq % 8 || ldk % 8 || ldv % 8 || ldo % 8 || lddo % 8 || lddq % 8 || lddk % 8 || lddv % 8)
     return hipErrorInvalidValue;
@@ -1162,11 +1190,11 @@ hipError_t pra_attn_bwd(const void* q, const void* k, const void* v, const void*
     if (Hq > PRE_MAXH) return hipErrorInvalidValue;
     const int grid = B * (S / PRE_QB);
     if (D == 128)
-      hipLaunchKernelGGL((bwd_pre_kernel<128>), dim3(grid), dim3(256), 0, st, (const __bf16*)o,
-                         (const __bf16*)dout, delta, B, S, Hq, ldo, lddo);
+      hipLaunchKernelGGL((bwd_pre_kernel<T, 128>), dim3(grid), dim3(256), 0, st, (const T*)o,
+                         (const T*)dout, delta, B, S, Hq, ldo, lddo);
     else
-      hipLaunchKernelGGL((bwd_pre_kernel<64>), dim3(grid), dim3(256), 0, st, (const __bf16*)o,
-                         (const __bf16*)dout, delta, B, S, Hq, ldo, lddo);
+      hipLaunchKernelGGL((bwd_pre_kernel<T, 64>), dim3(grid), dim3(256), 0, st, (const T*)o,
+                         (const T*)dout, delta, B, S, Hq, ldo, lddo);
   }
   {
     static const int nw_env = [] {
@@ -1185,18 +1213,18 @@ hipError_t pra_attn_bwd(const void* q, const void* k, const void* v, const void*
     if (p2 && nw_env == 0) {
       dim3 g1((S / 128) * Hkv * B);
 #define LAUNCH1(DD, CC)                                                                                       \
-  hipLaunchKernelGGL((bwd_dkdv_p2_kernel<DD, CC>), g1, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,    \
-                     (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dk, (__bf16*)dv, S, Hq, Hkv, ldq, \
-                     ldk, ldv, lddo, lddk, lddv, scale, sl2)
+  hipLaunchKernelGGL((bwd_dkdv_p2_kernel<T, DD, CC>), g1, dim3(256), 0, st, (const T*)q, (const T*)k,    \
+                     (const T*)v, (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Hq, Hkv, ldq, \
+                     ldk, ldv, lddo, lddk, lddv, scale, sl2, skv)
       if (D == 128) { if (causal) LAUNCH1(128, true); else LAUNCH1(128, false); }
       else { if (causal) LAUNCH1(64, true); else LAUNCH1(64, false); }
 #undef LAUNCH1
     } else {
     dim3 grid((S / (32 * nw)) * Hkv * B);
 #define LAUNCH(DD, CC, NWW)                                                                                     \
-  hipLaunchKernelGGL((bwd_dkdv_kernel<DD, CC, NWW>), grid, dim3(NWW * 64), 0, st, (const __bf16*)q,             \
-                     (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dk, (__bf16*)dv, \
-                     S, Hq, Hkv, ldq, ldk, ldv, lddo, lddk, lddv, scale, sl2, bwd_prio)
+  hipLaunchKernelGGL((bwd_dkdv_kernel<T, DD, CC, NWW>), grid, dim3(NWW * 64), 0, st, (const T*)q,             \
+                     (const T*)k, (const T*)v, (const T*)dout, lse, delta, (T*)dk, (T*)dv, \
+                     S, Hq, Hkv, ldq, ldk, ldv, lddo, lddk, lddv, scale, sl2, bwd_prio, skv)
     if (nw == 8) {
       if (D == 128) { if (causal) LAUNCH(128, true, 8); else LAUNCH(128, false, 8); }
       else { if (causal) LAUNCH(64, true, 8); else LAUNCH(64, false, 8); }
@@ -1215,16 +1243,17 @@ hipError_t pra_attn_bwd(const void* q, const void* k, const void* v, const void*
     const int nwq = (dq_env == 4 || S % 256) ? 4 : 8;
     dim3 grid(((S + 32 * nwq - 1) / (32 * nwq)) * Hq * B);
     const char* pipe_s = getenv("PRA_DQ_PIPE");  // read per call (tests switch it)
-    const bool pipe = pipe_s ? atoi(pipe_s) != 0 : true;
+    // the pipelined kernel has no key bound: padded non-causal sequences take the plain one
+    const bool pipe = (causal || skv >= S) && (pipe_s ? atoi(pipe_s) != 0 : true);
 #define LAUNCH(DD, CC, NWW)                                                                                     \
   if (pipe)                                                                                                     \
-  hipLaunchKernelGGL((bwd_dq_kernel<DD, CC, NWW, true>), grid, dim3(NWW * 64), 0, st, (const __bf16*)q,         \
-                     (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dq, S, Hq, Hkv,  \
-                     ldq, ldk, ldv, lddo, lddq, scale, sl2, bwd_prio);                                            \
+  hipLaunchKernelGGL((bwd_dq_kernel<T, DD, CC, NWW, true>), grid, dim3(NWW * 64), 0, st, (const T*)q,         \
+                     (const T*)k, (const T*)v, (const T*)dout, lse, delta, (T*)dq, S, Hq, Hkv,  \
+                     ldq, ldk, ldv, lddo, lddq, scale, sl2, bwd_prio, skv);                                            \
   else                                                                                                          \
-  hipLaunchKernelGGL((bwd_dq_kernel<DD, CC, NWW>), grid, dim3(NWW * 64), 0, st, (const __bf16*)q,               \
-                     (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dq, S, Hq, Hkv,  \
-                     ldq, ldk, ldv, lddo, lddq, scale, sl2, bwd_prio)
+  hipLaunchKernelGGL((bwd_dq_kernel<T, DD, CC, NWW>), grid, dim3(NWW * 64), 0, st, (const T*)q,               \
+                     (const T*)k, (const T*)v, (const T*)dout, lse, delta, (T*)dq, S, Hq, Hkv,  \
+                     ldq, ldk, ldv, lddo, lddq, scale, sl2, bwd_prio, skv)
     if (nwq == 8) {
       if (D == 128) { if (causal) LAUNCH(128, true, 8); else LAUNCH(128, false, 8); }
       else { if (causal) LAUNCH(64, true, 8); else LAUNCH(64, false, 8); }
@@ -1235,6 +1264,35 @@ hipError_t pra_attn_bwd(const void* q, const void* k, const void* v, const void*
 #undef LAUNCH
   }
   return hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+hipError_t pra_attn_fwd(int dtype, const void* q, const void* k, const void* v, void* o, float* lse, int B, int S,
+                        int Hq, int Hkv, int D, long ldq, long ldk, long ldv, long ldo, float scale, int causal,
+                        int skv, hipStream_t st) {
+  if (skv <= 0 || skv > S) return hipErrorInvalidValue;
+  if (dtype == pra::kBF16)
+    return attn_fwd_t<__bf16>(q, k, v, o, lse, B, S, Hq, Hkv, D, ldq, ldk, ldv, ldo, scale, causal, skv, st);
+  if (dtype == pra::kF16)
+    return attn_fwd_t<_Float16>(q, k, v, o, lse, B, S, Hq, Hkv, D, ldq, ldk, ldv, ldo, scale, causal, skv, st);
+  return hipErrorInvalidValue;
+}
+
+hipError_t pra_attn_bwd(int dtype, const void* q, const void* k, const void* v, const void* o, const void* dout,
+                        const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int S, int Hq, int Hkv,
+                        int D, long ldq, long ldk, long ldv, long ldo, long lddo, long lddq, long lddk, long lddv,
+                        float scale, int causal, int skv, hipStream_t st) {
+  if (skv <= 0 || skv > S) return hipErrorInvalidValue;
+  if (dtype == pra::kBF16)
+    return attn_bwd_t<__bf16>(q, k, v, o, dout, lse, delta, dq, dk, dv, B, S, Hq, Hkv, D, ldq, ldk, ldv, ldo, lddo,
+                              lddq, lddk, lddv, scale, causal, skv, st);
+  if (dtype == pra::kF16)
+    return attn_bwd_t<_Float16>(q, k, v, o, dout, lse, delta, dq, dk, dv, B, S, Hq, Hkv, D, ldq, ldk, ldv, ldo, lddo,
+                                lddq, lddk, lddv, scale, causal, skv, st);
+  return hipErrorInvalidValue;
 }
 
 }  // extern "C"

@@ -61,6 +61,13 @@ __device__ __forceinline__ void load8<__half>(const __half* __restrict__ p, floa
   for (int i = 0; i < 8; ++i) o[i] = __half2float(h[i]);
 }
 template <>
+__device__ __forceinline__ void load8<_Float16>(const _Float16* __restrict__ p, float (&o)[8]) {
+  uint4 raw = *reinterpret_cast<const uint4*>(p);
+  const _Float16* h = reinterpret_cast<const _Float16*>(&raw);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = (float)h[i];
+}
+template <>
 __device__ __forceinline__ void load8<float>(const float* __restrict__ p, float (&o)[8]) {
   float4 a = *reinterpret_cast<const float4*>(p);
   float4 b = *reinterpret_cast<const float4*>(p + 4);

@@ -51,11 +51,11 @@ hipError_t pra_grad_norm(int dtype, const void* x, long n, float* ws, float* out
 
 hipError_t pra_sum_slices(int dtype, const void* const* srcs, int nsrc, void* dst, long n, hipStream_t s);
 
-hipError_t pra_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int Hq,
+hipError_t pra_attn_fwd(int dtype, const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int Hq,
                         int Hkv, int D, long ldq, long ldk, long ldv, long ldo, float scale, int causal,
-                        hipStream_t st);
-hipError_t pra_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                        int skv, hipStream_t st);
+hipError_t pra_attn_bwd(int dtype, const void* q, const void* k, const void* v, const void* o, const void* dout,
                         const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int S, int Hq, int Hkv,
                         int D, long ldq, long ldk, long ldv, long ldo, long lddo, long lddq, long lddk, long lddv,
-                        float scale, int causal, hipStream_t st);
+                        float scale, int causal, int skv, hipStream_t st);
 }

@@ -43,3 +43,20 @@ def require_for(t) -> object:
     if os.environ.get("PYRECOVER_AMD_FORCE_REFERENCE") == "1":
         raise RuntimeError("PYRECOVER_AMD_FORCE_REFERENCE=1 is set but a GPU tensor reached a native op")
     return native()
+
+
+# dtypes the HIP kernels are instantiated for. GPU tensors of other dtypes (fp64) run the
+# plain-torch math of pyrecover_amd.ops.reference on the GPU, as do attention and the
+# transposing kernels for fp32 (their MFMA tiles are 16-bit).
+def hip(t) -> bool:
+    """True when ``t`` is a GPU tensor whose dtype the element-wise HIP kernels take (bf16/fp16/fp32)."""
+    import torch
+
+    return t.is_cuda and t.dtype in (torch.bfloat16, torch.float16, torch.float32)
+
+
+def hip16(t) -> bool:
+    """True for GPU bf16/fp16 tensors (the MFMA attention and the transposing kernels)."""
+    import torch
+
+    return t.is_cuda and t.dtype in (torch.bfloat16, torch.float16)

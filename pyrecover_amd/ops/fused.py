@@ -86,7 +86,7 @@ TN_WGRAD_WO = TN_WGRAD and os.environ.get("PYRECOVER_TN_WGRAD_WO", "1") == "1"
 
 
 def _tn_ok(t):
-    return (t.is_cuda and t.dim() == 2 and t.element_size() == 2 and t.stride(1) == 1 and t.size(0) % 64 == 0
+    return (_ext.hip16(t) and t.dim() == 2 and t.element_size() == 2 and t.stride(1) == 1 and t.size(0) % 64 == 0
             and t.size(1) % 64 == 0 and t.stride(0) % 8 == 0)
 
 
@@ -106,7 +106,7 @@ class _Embedding(torch.autograd.Function):
         ctx.slot = slot
         ctx.save_for_backward(ids)
         ctx.shape = weight.shape
-        if weight.is_cuda:
+        if _ext.hip(weight):
             return _ext.require_for(weight).embedding_fwd(ids.contiguous(), weight)
         return torch.nn.functional.embedding(ids, weight)
 
@@ -116,7 +116,7 @@ class _Embedding(torch.autograd.Function):
         slot = ctx.slot
         buf, acc = slot.begin(dout)
         V, D = ctx.shape
-        if dout.is_cuda:
+        if _ext.hip(dout):
             _ext.require_for(dout).embedding_bwd(ids.contiguous(), dout.contiguous(), buf.view(V, D), acc)
         else:
             g = buf.view(V, D)
@@ -139,7 +139,7 @@ class _AddRMSNorm(torch.autograd.Function):
     def forward(ctx, x, delta, weight, slot, eps):
         ctx.slot = slot
         ctx.has_delta = delta is not None
-        if x.is_cuda:
+        if _ext.hip(x):
             h, y, rstd = _ext.require_for(x).rmsnorm_fwd(x.contiguous(), delta.contiguous() if delta is not None else None,
                                                          weight, eps)
         else:
@@ -158,7 +158,7 @@ class _AddRMSNorm(torch.autograd.Function):
             dh, dy = None, grads[0]
         slot = ctx.slot
         buf, acc = slot.begin(dy)
-        if dy.is_cuda:
+        if _ext.hip(dy):
             dx = _ext.require_for(dy).rmsnorm_bwd(dy.contiguous(), h, weight, rstd,
                                                   dh.contiguous() if dh is not None else None, buf, acc)
         else:
@@ -188,7 +188,7 @@ class _AddLayerNorm(torch.autograd.Function):
         ctx.slot = slot
         ctx.has_delta = delta is not None
         ctx.eps = eps
-        if x.is_cuda:
+        if _ext.hip(x):
             h, y, mean, rstd = _ext.require_for(x).layernorm_fwd(
                 x.contiguous(), delta.contiguous() if delta is not None else None, weight, bias, eps)
         else:
@@ -207,7 +207,7 @@ class _AddLayerNorm(torch.autograd.Function):
         slot = ctx.slot
         buf, acc = slot.begin(dy)
         D = h.shape[-1]
-        if dy.is_cuda:
+        if _ext.hip(dy):
             dx = _ext.require_for(dy).layernorm_bwd(dy.contiguous(), h, weight, mean, rstd,
                                                     dh.contiguous() if dh is not None else None, buf, acc)
         else:
@@ -235,20 +235,26 @@ def add_layer_norm(x, delta, weight, bias, slot, eps):
 
 # ---------------------------------------------------------------------------------------
 def _attn_fwd(q, k, v, scale, causal):
-    if q.is_cuda:
+    """HIP flash attention for bf16/fp16 GPU tensors (any S: the binding zero-pads sequences
+    that do not tile); otherwise torch SDPA in fp32 (fp64 for fp64 inputs), as the reference's
+    non-flash path (reference model.py:192, 227). Returns (o, lse or None)."""
+    if _ext.hip16(q):
         return _ext.require_for(q).attn_fwd(q, k, v, scale, causal)
-    o, lse = ref.attention_lse_ref(q, k, v, causal, scale)
-    return o.to(q.dtype).contiguous(), lse
+    ct = torch.promote_types(q.dtype, torch.float32)
+    with torch.no_grad():
+        o = ref.attention_ref(q.to(ct), k.to(ct), v.to(ct), causal, scale)
+    return o.to(q.dtype).contiguous(), None
 
 
 def _attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, causal):
-    if q.is_cuda:
+    if _ext.hip16(q):
         _ext.require_for(q).attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, causal)
         return
+    ct = torch.promote_types(q.dtype, torch.float32)
     with torch.enable_grad():
-        qq, kk, vv = (t.detach().float().requires_grad_() for t in (q, k, v))
-        out, _ = ref.attention_lse_ref(qq, kk, vv, causal, scale)
-        gq, gk, gv = torch.autograd.grad(out, (qq, kk, vv), do.float())
+        qq, kk, vv = (t.detach().to(ct).requires_grad_() for t in (q, k, v))
+        out = ref.attention_ref(qq, kk, vv, causal, scale)
+        gq, gk, gv = torch.autograd.grad(out, (qq, kk, vv), do.to(ct))
     dq.copy_(gq)
     dk.copy_(gk)
     dv.copy_(gv)
@@ -266,7 +272,7 @@ class _AttentionBlock(torch.autograd.Function):
         x2 = x.reshape(T, dim)
         qkv = torch.mm(x2, w_qkv.t())
         nq, nk = Hq * D, Hkv * D
-        if qkv.is_cuda:
+        if _ext.hip(qkv):
             _ext.require_for(qkv).rope_(qkv, nq + nk, tab, D, S, 0, False)
         else:
             ref.rope_inplace_2d(qkv, nq + nk, tab, D, S)
@@ -315,7 +321,7 @@ class _AttentionBlock(torch.autograd.Function):
             dx = torch.mm(dqkv, w_qkv_t.t()) if w_qkv_t is not None else torch.mm(dqkv, w_qkv)
             slot_qkv.mm_(dqkvT, C.transpose2d(x2).t(), tuple(w_qkv.shape))
         else:
-            if dqkv.is_cuda:
+            if _ext.hip(dqkv):
                 _ext.require_for(dqkv).rope_(dqkv, nq + nk, tab, D, S, 0, True)
             else:
                 ref.rope_inplace_2d(dqkv, nq + nk, tab, D, S, inverse=True)
@@ -333,15 +339,15 @@ def attention_block(x, w_qkv, w_o, slot_qkv, slot_o, tab, dims, params, w_t=None
 
 # ---------------------------------------------------------------------------------------
 def _swiglu_fwd(gu):
-    if gu.is_cuda:
+    if _ext.hip(gu):
         return _ext.require_for(gu).swiglu_fwd(gu)
     F = gu.shape[1] // 2
-    g, u = gu[:, :F].float(), gu[:, F:].float()
-    return (torch.nn.functional.silu(g).to(gu.dtype).float() * u).to(gu.dtype)
+    g, u = ref.up(gu[:, :F]), ref.up(gu[:, F:])
+    return (ref.up(torch.nn.functional.silu(g).to(gu.dtype)) * u).to(gu.dtype)
 
 
 def _swiglu_bwd_(da, gu):
-    if gu.is_cuda:
+    if _ext.hip(gu):
         return _ext.require_for(gu).swiglu_bwd(da, gu, gu)
     F = gu.shape[1] // 2
     dg, du = ref.swiglu_bwd_ref(da, gu[:, :F], gu[:, F:])
@@ -416,12 +422,11 @@ class _LinearCrossEntropy(torch.autograd.Function):
         h2 = h.reshape(-1, h.shape[-1])
         lab = labels.reshape(-1).contiguous()
         logits = torch.mm(h2, w_out.t())
-        if logits.is_cuda:
+        if _ext.hip(logits):
             lse, _, stats = _ext.require_for(logits).xent_fwd(logits, lab, ignore_index)
             loss = stats[0]
         else:
-            lf = logits.float()
-            lse = torch.logsumexp(lf, dim=-1)
+            lse = torch.logsumexp(ref.up(logits), dim=-1)
             stats = None
             loss = ref.cross_entropy_ref(logits, lab, ignore_index)
         ctx.save_for_backward(h2, logits, lab, lse, w_out, stats if stats is not None else lse)
@@ -433,16 +438,16 @@ class _LinearCrossEntropy(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dloss):
         h2, logits, lab, lse, w_out, stats = ctx.saved_tensors
-        if logits.is_cuda:
+        if _ext.hip(logits):
             g = dloss.reshape(1).float().contiguous()
             _ext.require_for(logits).xent_bwd_(logits, lab, lse, stats, g, ctx.ignore_index)
             dlogits = logits
         else:
             valid = lab.ne(ctx.ignore_index)
             n = valid.sum().clamp_min(1)
-            p = torch.softmax(logits.float(), dim=-1)
-            p[torch.arange(lab.numel()), lab.clamp_min(0)] -= valid.float()
-            p = p * valid.float().unsqueeze(1) * (dloss.float() / n)
+            p = torch.softmax(ref.up(logits), dim=-1)
+            p[torch.arange(lab.numel(), device=p.device), lab.clamp_min(0)] -= valid.to(p.dtype)
+            p = p * valid.to(p.dtype).unsqueeze(1) * (dloss.to(p.dtype) / n)
             dlogits = p.to(logits.dtype)
         dh = torch.mm(dlogits, ctx.w_t.t()) if ctx.w_t is not None else torch.mm(dlogits, w_out)
         _wgrad_into(ctx.slot, dlogits, h2, tuple(w_out.shape))

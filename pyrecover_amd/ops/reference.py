@@ -26,10 +26,15 @@ def rope_table(freqs_cis: torch.Tensor) -> torch.Tensor:
     return torch.view_as_real(freqs_cis).contiguous()
 
 
+def up(x: torch.Tensor) -> torch.Tensor:
+    """Opmath of ``x``: fp32 for 16-bit/fp32 tensors, fp64 for fp64 (fp64 models stay fp64)."""
+    return x.to(torch.promote_types(x.dtype, torch.float32))
+
+
 # ---------------------------------------------------------------------------------------
 def rmsnorm_ref(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
     """reference model.py:44-49"""
-    xf = x.float()
+    xf = up(x)
     out = (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)).type_as(x)
     return out * w
 
@@ -37,7 +42,7 @@ def rmsnorm_ref(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
 def rmsnorm_fwd(x, delta, w, eps):
     """(h, y, rstd) with h = round(x + delta) when delta is given."""
     h = x if delta is None else (x + delta)
-    hf = h.float()
+    hf = up(h)
     rstd = torch.rsqrt(hf.pow(2).mean(-1) + eps)
     y = (hf * rstd.unsqueeze(-1)).to(h.dtype) * w
     return h, y, rstd.reshape(-1)
@@ -46,12 +51,12 @@ def rmsnorm_fwd(x, delta, w, eps):
 def rmsnorm_bwd(dy, h, w, rstd, dres):
     """returns (dx, dw_fp32) with the same rounding points as the HIP kernel."""
     D = h.shape[-1]
-    hf = h.float().reshape(-1, D)
-    dyf = dy.float().reshape(-1, D)
+    hf = up(h).reshape(-1, D)
+    dyf = up(dy).reshape(-1, D)
     r = rstd.reshape(-1, 1)
-    nb = (hf * r).to(h.dtype).float()
+    nb = up((hf * r).to(h.dtype))
     dw = (dyf * nb).sum(0)
-    g = (dyf * w.float()).to(h.dtype).float()
+    g = up((dyf * up(w)).to(h.dtype))
     dot = (g * hf).sum(-1, keepdim=True)
     dx = (r * (g - hf * (r * r * dot / D))).to(h.dtype)
     if dres is not None:
@@ -63,7 +68,7 @@ def rope_inplace_2d(x2d: torch.Tensor, ncols: int, tab: torch.Tensor, head_dim: 
                     inverse: bool = False):
     """Rotate the first `ncols` columns of every row (heads of size head_dim), interleaved pairs."""
     T = x2d.shape[0]
-    v = x2d[:, :ncols].float().reshape(T // seq_len, seq_len, ncols // head_dim, head_dim // 2, 2)
+    v = up(x2d[:, :ncols]).reshape(T // seq_len, seq_len, ncols // head_dim, head_dim // 2, 2)
     c = tab[:seq_len, :, 0].view(1, seq_len, 1, head_dim // 2)
     s = tab[:seq_len, :, 1].view(1, seq_len, 1, head_dim // 2)
     if inverse:
@@ -75,8 +80,8 @@ def rope_inplace_2d(x2d: torch.Tensor, ncols: int, tab: torch.Tensor, head_dim: 
 
 def apply_rotary_emb_ref(xq, xk, freqs_cis):
     """reference model.py:101-127 ([B, S, H, D] tensors)"""
-    xq_ = torch.view_as_complex(xq.float().reshape(*xq.shape[:-1], -1, 2))
-    xk_ = torch.view_as_complex(xk.float().reshape(*xk.shape[:-1], -1, 2))
+    xq_ = torch.view_as_complex(up(xq).reshape(*xq.shape[:-1], -1, 2))
+    xk_ = torch.view_as_complex(up(xk).reshape(*xk.shape[:-1], -1, 2))
     fc = freqs_cis[: xq.shape[1]].view(1, xq.shape[1], 1, xq_.shape[-1])
     xq_out = torch.view_as_real(xq_ * fc).flatten(3)
     xk_out = torch.view_as_real(xk_ * fc).flatten(3)
@@ -100,9 +105,9 @@ def attention_lse_ref(q, k, v, causal=True, scale=None):
     B, S, Hq, D = q.shape
     Hkv = k.shape[2]
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
-    kk = k.float().repeat_interleave(Hq // Hkv, dim=2)
-    vv = v.float().repeat_interleave(Hq // Hkv, dim=2)
-    s = torch.einsum("bqhd,bkhd->bhqk", q.float(), kk) * scale
+    kk = up(k).repeat_interleave(Hq // Hkv, dim=2)
+    vv = up(v).repeat_interleave(Hq // Hkv, dim=2)
+    s = torch.einsum("bqhd,bkhd->bhqk", up(q), kk) * scale
     if causal:
         m = torch.ones(S, S, dtype=torch.bool, device=q.device).triu(1)
         s = s.masked_fill(m, float("-inf"))
@@ -118,10 +123,10 @@ def swiglu_ref(g, u):
 
 
 def swiglu_bwd_ref(dy, g, u):
-    gf, uf, dyf = g.float(), u.float(), dy.float()
+    gf, uf, dyf = up(g), up(u), up(dy)
     sg = torch.sigmoid(gf)
-    a = (gf * sg).to(g.dtype).float()
-    da = (dyf * uf).to(g.dtype).float()
+    a = up((gf * sg).to(g.dtype))
+    da = up((dyf * uf).to(g.dtype))
     du = dyf * a
     dg = da * sg * (1 + gf * (1 - sg))
     return dg.to(g.dtype), du.to(g.dtype)
@@ -130,6 +135,6 @@ def swiglu_bwd_ref(dy, g, u):
 def cross_entropy_ref(logits, labels, ignore_index: int = -100):
     """reference train.py:253,263-266: sum-reduced CE on fp32 logits / #non-ignored labels."""
     n = labels.ne(ignore_index).sum()
-    loss = F.cross_entropy(logits.flatten(0, -2).float(), labels.flatten(), reduction="sum",
+    loss = F.cross_entropy(up(logits.flatten(0, -2)), labels.flatten(), reduction="sum",
                            ignore_index=ignore_index)
     return loss / n

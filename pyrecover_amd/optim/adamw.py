@@ -93,7 +93,7 @@ class FlatAdamW(torch.optim.AdamW):
     def _update_range(self, lo, hi):
         f = self.flat
         lr, b1, b2, eps, wd, bc1, bc2_sqrt = self._coeffs()
-        if f.data.is_cuda:
+        if _ext.hip(f.data):
             _ext.require_for(f.data).adamw_flat_(f.data[lo:hi], f.grad[lo:hi], self.exp_avg[lo:hi],
                                                  self.exp_avg_sq[lo:hi], lr, b1, b2, eps, wd, bc1, bc2_sqrt,
                                                  self.grad_scale, self.grad_scale_dev, self.hyper)
@@ -165,7 +165,7 @@ class FlatAdamW(torch.optim.AdamW):
         bc1 = 1.0 - b1 ** self._step
         bc2_sqrt = math.sqrt(1.0 - b2 ** self._step)
         f = self.flat
-        if f.data.is_cuda:
+        if _ext.hip(f.data):
             _ext.require_for(f.data).adamw_flat_(f.data, f.grad, self.exp_avg, self.exp_avg_sq, lr, b1, b2, eps, wd,
                                                  bc1, bc2_sqrt, self.grad_scale, self.grad_scale_dev, self.hyper)
             f.refresh_transposed()
@@ -178,10 +178,11 @@ class FlatAdamW(torch.optim.AdamW):
         hi = f.numel if hi is None else hi
         gs = self.grad_scale * (float(self.grad_scale_dev[0]) if self.grad_scale_dev is not None else 1.0)
         pd, gd, md, vd = f.data[lo:hi], f.grad[lo:hi], self.exp_avg[lo:hi], self.exp_avg_sq[lo:hi]
-        p = pd.float()
-        gr = gd.float() * gs
-        m = md.float()
-        v = vd.float()
+        ct = torch.promote_types(pd.dtype, torch.float32)  # fp32 opmath; fp64 models stay fp64
+        p = pd.to(ct)
+        gr = gd.to(ct) * gs
+        m = md.to(ct)
+        v = vd.to(ct)
         p.mul_(1 - lr * wd)
         m.lerp_(gr, 1 - b1)
         v.mul_(b2).addcmul_(gr, gr, value=1 - b2)

@@ -426,9 +426,9 @@ def train(args):
 
 def _clip_coef(flat, max_norm: float, pre_scale: float):
     """Device-side clip coefficient min(1, max_norm / ||g||) over the flat (reduced) gradient."""
-    if flat.grad.is_cuda:
-        from . import _ext
+    from . import _ext
 
+    if _ext.hip(flat.grad):
         return _ext.native().grad_norm(flat.grad, max_norm, pre_scale)[1:2]
-    norm = flat.grad.float().norm() * pre_scale
-    return torch.clamp(max_norm / (norm + 1e-6), max=1.0).reshape(1)
+    norm = flat.grad.to(torch.promote_types(flat.grad.dtype, torch.float32)).norm() * pre_scale
+    return torch.clamp(max_norm / (norm + 1e-6), max=1.0).reshape(1).float()

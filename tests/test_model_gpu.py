@@ -28,9 +28,14 @@ def ref_forward(m, tok):
     return h @ m.output.weight.t()
 
 
-@pytest.mark.parametrize("preset,over", [("llama-micro", {}), ("llama-tiny", {}),
-                                         ("gpt2-small", {"n_layers": 2, "vocab_size": 1024})])
-def test_model_grads_vs_fp32_reference(cuda, preset, over):
+@pytest.mark.parametrize("preset,over,dtype", [("llama-micro", {}, torch.bfloat16), ("llama-tiny", {}, torch.bfloat16),
+                                               ("gpt2-small", {"n_layers": 2, "vocab_size": 1024}, torch.bfloat16),
+                                               ("llama-tiny", {"n_kv_heads": 2}, torch.float16),
+                                               ("llama-micro", {}, torch.float32),
+                                               ("llama-micro", {}, torch.float64)])
+def test_model_grads_vs_fp32_reference(cuda, preset, over, dtype):
+    """Every --model-dtype trains on the GPU: bf16/fp16 on the HIP kernels, fp32 on the HIP
+    element-wise kernels + torch attention, fp64 on torch math (reference utils.py:11-16)."""
     torch.manual_seed(0)
     a = get_preset(preset, seq_len=256, **over)
     cpu = Transformer(a)
@@ -44,16 +49,18 @@ def test_model_grads_vs_fp32_reference(cuda, preset, over):
 
     gpu = Transformer(a)
     gpu.load_state_dict(cpu.state_dict())
-    gpu = gpu.to(cuda, torch.bfloat16)
+    gpu = gpu.to(cuda, dtype)
     flat = gpu.flatten_()
     flat.zero_grad()
     loss = gpu(tok.to(cuda), labels=lab.to(cuda))
     loss.backward()
-    assert abs(loss.item() - loss_ref.item()) < 2e-2 * loss_ref.item()
+    tol = {torch.float32: 1e-3, torch.float64: 1e-4}.get(dtype, 5e-2)
+    assert abs(loss.item() - loss_ref.item()) < max(tol, 2e-3) * loss_ref.item()
     for n, p in gpu.named_parameters():
+        assert p.grad.dtype == dtype
         g, r = p.grad.float().cpu(), gref[n]
         rel = ((g - r).norm() / r.norm().clamp_min(1e-12)).item()
-        assert rel < 5e-2, (n, rel)
+        assert rel < tol, (n, rel)
 
 
 def _train_steps(cuda, overlap, steps=3, preset="llama-tiny", seed=0, recompute=False):
@@ -201,3 +208,26 @@ def test_weight_shadows_off_gives_the_same_gradients(cuda, monkeypatch):
         grads.append(flat.grad.float().clone())
     rel = ((grads[0] - grads[1]).norm() / grads[0].norm()).item()
     assert rel < 1e-2, rel
+
+
+@pytest.mark.parametrize("dtype", ["fp16", "fp32", "fp64"])
+def test_train_py_model_dtypes(cuda, tmp_path, dtype):
+    """train.py --model-dtype {fp16,fp32,fp64} on the GPU: a few steps, finite loss, a checkpoint
+    that resumes (reference utils.py:176-181, train.py:100-101)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    args = [sys.executable, os.path.join(root, "train.py"), "--model-preset", "llama-tiny", "--synthetic-data",
+            "--batch-size", "2", "--sequence-length", "200", "--training-steps", "4", "--checkpoint-frequency", "2",
+            "--logging-frequency", "1", "--num-workers", "0", "--model-dtype", dtype,
+            "--checkpoint-dir", str(tmp_path), "--experiment_name", "dt"]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    assert "Loss: nan" not in r.stdout + r.stderr
+    args2 = list(args)
+    args2[args2.index("--training-steps") + 1] = "6"
+    r2 = subprocess.run(args2 + ["--resume-from-checkpoint", "latest"], capture_output=True, text=True, timeout=300,
+                        cwd=root)
+    assert r2.returncode == 0, (r2.stdout + r2.stderr)[-4000:]
