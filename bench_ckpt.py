@@ -24,6 +24,11 @@ import time
 import torch
 
 
+def _wstats(core):
+    last = core.WRITE_STATS.get("last", {})
+    return {k: (round(v, 3) if isinstance(v, float) else v) for k, v in last.items() if k not in ("error", "md5")}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="llama2-7b")
@@ -35,7 +40,7 @@ def main():
     ap.add_argument("--formats", default="vanilla,async,sharded")
     args = ap.parse_args()
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    from pyrecover_amd.ckpt import core
+    from pyrecover_amd.ckpt import core, fastload
     from pyrecover_amd.ckpt.sharded import load_ckpt_distributed, save_ckpt_distributed
     from pyrecover_amd.ckpt.vanilla import load_ckpt_vanilla, save_ckpt_vanilla
     from pyrecover_amd.config import get_preset
@@ -84,7 +89,7 @@ def main():
     os.makedirs(args.dir, exist_ok=True)
     out = {"metric": "checkpoint save+resume wall-clock", "model": f"{args.model}-shape",
            "params": model.num_params(), "state_bytes": 3 * flat.state_bytes(), "step_s": round(step_s, 3),
-           "dir": args.dir}
+           "dir": args.dir, "whole_file_md5": os.environ.get("PYRECOVER_WHOLE_MD5", "1") != "0"}
     ref_params = flat.data.clone()
     ref_v = opt.exp_avg_sq.clone()
     formats = args.formats.split(",")
@@ -99,6 +104,7 @@ def main():
         t0 = time.perf_counter()
         save_ckpt_vanilla(model, opt, sched, None, 2, 1, p, max_keep=0, verify=args.verify)
         out["vanilla_save_s"] = round(time.perf_counter() - t0, 3)
+        out["vanilla_write"] = _wstats(core)
         out["vanilla_file_gib"] = round(os.path.getsize(p) / 2**30, 3)
         del model, opt
         torch.cuda.empty_cache()
@@ -108,6 +114,8 @@ def main():
         load_ckpt_vanilla(m2, opt2, sched2, None, p, verify=args.verify)
         torch.cuda.synchronize()
         out["vanilla_load_s"] = round(time.perf_counter() - t0, 3)
+        out["vanilla_load_native"] = {k: (round(v, 3) if isinstance(v, float) else v)
+                                      for k, v in fastload.LAST_STATS.items()}
         out["vanilla_bit_exact"] = bool(torch.equal(flat2.data, ref_params) and torch.equal(opt2.exp_avg_sq, ref_v))
         model, flat, opt, sched = m2, flat2, opt2, sched2
         red = GradReducer(flat)
@@ -146,6 +154,7 @@ def main():
         t0 = time.perf_counter()
         save_ckpt_distributed(model, opt, sched, None, 4, 1, d, max_keep=0)
         out["sharded_save_s"] = round(time.perf_counter() - t0, 3)
+        out["sharded_write"] = _wstats(core)
         del model, opt
         torch.cuda.empty_cache()
         m2, flat2, opt2, sched2 = check_loaded("sharded")
@@ -154,6 +163,8 @@ def main():
         load_ckpt_distributed(m2, opt2, sched2, None, d)
         torch.cuda.synchronize()
         out["sharded_load_s"] = round(time.perf_counter() - t0, 3)
+        out["sharded_load_native"] = {k: (round(v, 3) if isinstance(v, float) else v)
+                                      for k, v in fastload.LAST_STATS.items()}
         out["sharded_bit_exact"] = bool(torch.equal(flat2.data, ref_params) and torch.equal(opt2.exp_avg_sq, ref_v))
         shutil.rmtree(d, ignore_errors=True)
 

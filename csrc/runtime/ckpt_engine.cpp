@@ -66,11 +66,45 @@ void register_ckpt_engine(py::module& m) {
         d["bytes"] = r.bytes;
         d["seconds"] = r.seconds;
         d["stage_wait_seconds"] = r.stage_wait_seconds;
+        d["layout_seconds"] = r.layout_seconds;
+        d["write_seconds"] = r.write_seconds;
+        d["fsync_seconds"] = r.fsync_seconds;
+        d["writers"] = r.writers;
+        d["direct"] = r.direct;
         py::list items;
         for (auto& it : r.items) items.append(py::make_tuple(it.first, it.second));
         d["items"] = items;
+        py::list recs;
+        for (auto& rc : r.records) recs.append(py::make_tuple(rc.name, rc.data_off, rc.nbytes));
+        d["records"] = recs;
+        d["seg_bytes"] = r.seg_bytes;
+        d["seg_md5"] = r.seg_md5;
         return d;
       });
+  py::class_<Reader>(m, "CkptReader")
+      .def(py::init<int>())
+      .def("read",
+           [](Reader& rd, const std::string& path, const std::vector<std::tuple<uint64_t, uint64_t, uintptr_t>>& items,
+              const std::vector<int64_t>& hash_segs, int threads, bool direct) {
+             // items: (file offset, nbytes, destination pointer: device memory, or host memory in CPU mode)
+             std::vector<ReadItem> v;
+             v.reserve(items.size());
+             for (auto& t : items) v.push_back({std::get<0>(t), std::get<1>(t), std::get<2>(t)});
+             ReadResult r;
+             {
+               py::gil_scoped_release nogil;
+               r = rd.read(path, std::move(v), hash_segs, threads, direct);
+             }
+             py::dict d;
+             d["ok"] = r.ok;
+             d["error"] = r.error;
+             d["seg_md5"] = r.seg_md5;
+             d["bytes_read"] = r.bytes_read;
+             d["seconds"] = r.seconds;
+             d["direct"] = r.direct;
+             return d;
+           });
+  m.attr("MD5PARTS_SEGMENT_BYTES") = py::int_(kSegBytes);
   m.def("md5_file", &md5_file, py::call_guard<py::gil_scoped_release>());
   m.def("crc32_bytes", [](py::bytes b) {
     std::string s = b;

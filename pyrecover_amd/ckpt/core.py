@@ -256,6 +256,7 @@ class Job:
             if not self.result["ok"]:
                 raise RuntimeError(f"checkpoint write to {self.path} failed: {self.result['error']}")
             WRITE_STATS["max_seconds"] = max(WRITE_STATS["max_seconds"], float(self.result.get("seconds", 0.0)))
+            WRITE_STATS["last"] = {k: v for k, v in self.result.items() if k not in ("items", "records", "seg_md5")}
             if self.on_done is not None:
                 self.on_done(self.result)
         return self.result
@@ -375,8 +376,9 @@ def apply_retention(base: Path, max_keep: int, distributed: bool):
                 shutil.rmtree(old)
             else:
                 old.unlink()
-                md5 = Path(str(old) + ".md5")
-                if md5.exists():
-                    md5.unlink()
+                for side in (".md5", ".md5parts"):
+                    sp = Path(str(old) + side)
+                    if sp.exists():
+                        sp.unlink()
         except FileNotFoundError:
             pass

@@ -169,8 +169,15 @@ def finalize_pending():
         if len(res["items"]) != len(pend["meta"]):
             raise RuntimeError(f"shard {pend['fname']} of {pend['path']}: {len(res['items'])} records written, "
                                f"{len(pend['meta'])} expected")
-        local = [(k, kind, dt, shape, pend["fname"], off, ln)
-                 for (k, kind, dt, shape), (off, ln) in zip(pend["meta"], res["items"])]
+        # payload offset of each tensor blob's "data/0" record (the fast loader reads only those bytes)
+        data0 = {}
+        for name, doff, _ in res["records"]:
+            if name.endswith("/data/0"):
+                for i, (off, ln) in enumerate(res["items"]):
+                    if off <= doff < off + ln:
+                        data0[i] = doff
+        local = [(k, kind, dt, shape, pend["fname"], off, ln, data0.get(i))
+                 for i, ((k, kind, dt, shape), (off, ln)) in enumerate(zip(pend["meta"], res["items"]))]
         gathered = [local]
         if pend["distributed"]:
             gathered = [None] * pend["world"]
@@ -190,7 +197,7 @@ def _write_metadata(path: Path, items, entries):
                                                        TensorStorageMetadata)
 
     sd_meta, storage, planner, manifest = {}, {}, {}, {}
-    for (k, kind, dt, shape, fname, off, ln) in entries:
+    for (k, kind, dt, shape, fname, off, ln, data_off) in entries:
         val, keypath = items[k]
         planner[k] = keypath
         if kind == "tensor":
@@ -201,6 +208,8 @@ def _write_metadata(path: Path, items, entries):
                                                                             sizes=size)])
             storage[MetadataIndex(fqn=k, offset=torch.Size([0] * len(size)), index=0)] = _StorageInfo(fname, off, ln)
             manifest[k] = {"file": fname, "offset": off, "length": ln, "dtype": dt, "shape": shape}
+            if data_off is not None:
+                manifest[k]["data_offset"] = data_off
         else:
             sd_meta[k] = BytesStorageMetadata()
             storage[MetadataIndex(fqn=k)] = _StorageInfo(fname, off, ln)
@@ -264,18 +273,51 @@ def _tensor_from_manifest(path: Path, ent) -> torch.Tensor:
                 head = head[:pos] + f.read(4096)
 
 
-def read_sharded_state(path: str) -> Dict[str, Any]:
-    """Rebuild the nested state dict (CPU tensors) of a sharded checkpoint (ours or dcp's)."""
+class _MetadataUnpickler(pickle.Unpickler):
+    """Unpickles a dcp ``.metadata`` file while refusing every global that is not part of the dcp
+    metadata schema (dataclasses of torch.distributed.checkpoint, torch.Size, dtypes, containers),
+    so a crafted checkpoint directory cannot execute code on load."""
+
+    _MODULES = ("torch.distributed.checkpoint.metadata", "torch.distributed.checkpoint.filesystem",
+                "torch.distributed.checkpoint.planner")
+    _GLOBALS = {("torch", "Size"), ("collections", "OrderedDict"), ("builtins", "set"), ("builtins", "frozenset"),
+                ("builtins", "slice"), ("copyreg", "_reconstructor"), ("builtins", "object"), ("enum", "Enum"),
+                ("torch._utils", "_rebuild_tensor_v2"), ("torch.storage", "_load_from_bytes"),
+                ("torch", "device"), ("torch", "memory_format"), ("torch", "layout"),
+                ("torch.serialization", "_get_layout"), ("pathlib", "PosixPath"), ("pathlib", "PurePosixPath")}
+
+    def find_class(self, module, name):
+        if module in self._MODULES or (module, name) in self._GLOBALS:
+            return super().find_class(module, name)
+        if module == "torch" and isinstance(getattr(torch, name, None), (torch.dtype, torch.layout,
+                                                                         torch.memory_format)):
+            return super().find_class(module, name)
+        raise pickle.UnpicklingError(f"checkpoint metadata references {module}.{name}, which is not allowed")
+
+
+def read_metadata(path) -> Any:
+    with open(Path(path) / ".metadata", "rb") as f:
+        return _MetadataUnpickler(f).load()
+
+
+def read_tensor(p: Path, ent) -> torch.Tensor:
+    return _tensor_from_manifest(p, ent)
+
+
+def read_sharded_state(path: str, skip=()) -> Dict[str, Any]:
+    """Rebuild the nested state dict (CPU tensors) of a sharded checkpoint (ours or dcp's).
+    Entries named in ``skip`` are not read (None placeholders; the fast loader places them)."""
     p = Path(path)
-    with open(p / ".metadata", "rb") as f:
-        md = pickle.load(f)  # a dcp Metadata object (written by us or by torch.distributed.checkpoint)
+    md = read_metadata(p)  # a dcp Metadata object (written by us or by torch.distributed.checkpoint)
     manifest = {}
     if (p / MANIFEST).exists():
         manifest = json.loads((p / MANIFEST).read_text())
     flat: Dict[str, Any] = {}
     for idx, sinfo in md.storage_data.items():
         k = idx.fqn
-        if k in manifest:
+        if k in skip:
+            flat[k] = None
+        elif k in manifest:
             flat[k] = _tensor_from_manifest(p, manifest[k])
         else:
             flat[k] = _load_value(p, sinfo)
@@ -314,22 +356,8 @@ def _fix_lists(o):
     return o
 
 
-def _set_in(container, key, value):
-    container[key] = value
-
-
-def load_ckpt_distributed(model, optimizer, lr_scheduler=None, sampler=None, checkpoint_path: str = "latest",
-                          experiment_dir: str = ".", verify: bool = True, is_distributed: bool = False,
-                          rank: int = 0) -> Tuple[int, int]:
-    if is_distributed:
-        dist.barrier()
-    core.wait_all()
-    finalize_pending()
-    if checkpoint_path == "latest":
-        checkpoint_path = core.get_latest_checkpoint(str(experiment_dir), distributed=True)
-        if checkpoint_path is None:
-            raise RuntimeError(f"No checkpoint found in {experiment_dir}")
-    st = read_sharded_state(checkpoint_path)
+def build_ckpt(st: Dict[str, Any]) -> Dict[str, Any]:
+    """dcp-layout state -> the vanilla checkpoint dict layout (reference checkpoint.py:254-258)."""
     model_sd = st.get("model", {})
     opt_sd = st.get("optimizer")
     if opt_sd is not None:
@@ -344,9 +372,51 @@ def load_ckpt_distributed(model, optimizer, lr_scheduler=None, sampler=None, che
         ckpt["sampler_state"] = st["sampler"]
     if "pyrecover_state" in st:
         ckpt["pyrecover_state"] = st["pyrecover_state"]
-    from .vanilla import load_state_into
+    return ckpt
 
-    epoch, step = load_state_into(model, optimizer, lr_scheduler, sampler, ckpt)
+
+def fill_value(ckpt: Dict[str, Any], fqn: str, value):
+    """Put a dcp FQN's value into a :func:`build_ckpt` dict."""
+    parts = fqn.split(".")
+    if parts[0] == "model":
+        ckpt["model"][".".join(parts[1:])] = value
+    elif parts[:2] == ["optimizer", "state"]:
+        ckpt["optimizer"]["state"][int(parts[2])][".".join(parts[3:])] = value
+    else:
+        raise KeyError(fqn)
+
+
+def load_ckpt_distributed(model, optimizer, lr_scheduler=None, sampler=None, checkpoint_path: str = "latest",
+                          experiment_dir: str = ".", verify: bool = True, is_distributed: bool = False,
+                          rank: int = 0) -> Tuple[int, int]:
+    if is_distributed:
+        dist.barrier()
+    core.wait_all()
+    finalize_pending()
+    if checkpoint_path == "latest":
+        checkpoint_path = core.get_latest_checkpoint(str(experiment_dir), distributed=True)
+        if checkpoint_path is None:
+            raise RuntimeError(f"No checkpoint found in {experiment_dir}")
+    from . import fastload
+
+    stats = None
+    try:
+        plan = fastload.plan_sharded(checkpoint_path, model, optimizer) if fastload.ENABLED else None
+    except (ValueError, KeyError, OSError) as e:  # not our layout: generic path
+        logger.info(f"sharded fast load not applicable ({e}); using the generic reader")
+        plan = None
+    if plan is not None:
+        ckpt, pl = plan
+        stats = fastload.execute(pl, fastload.flat_buffers(model, optimizer), False, None, None, is_distributed)
+        epoch, step = fastload.finish_state(model, optimizer, lr_scheduler, sampler, ckpt, pl)
+    else:
+        from .vanilla import load_state_into
+
+        ckpt = build_ckpt(read_sharded_state(checkpoint_path))
+        epoch, step = load_state_into(model, optimizer, lr_scheduler, sampler, ckpt)
+    if stats is not None:
+        logger.info(f"native read: {stats['bytes_read'] / 2**30:.2f} GiB in {stats['read_s']:.2f}s"
+                    + (f", all-gather {stats['allgather_s']:.2f}s" if "allgather_s" in stats else ""))
     if is_distributed:
         dist.barrier()
     logger.info(f"Distributed checkpoint loaded from {checkpoint_path} (epoch {epoch}, step {step})")

@@ -66,7 +66,7 @@ def save_ckpt_vanilla(model, optimizer, lr_scheduler=None, sampler=None, step: i
 
 
 def verify_checkpoint(path: str) -> Tuple[bool, str]:
-    """Compare the file's md5 with its ``.md5`` sidecar (streaming, native)."""
+    """Compare the file's md5 with its ``.md5`` sidecar (streaming, native; whole file)."""
     try:
         want = Path(str(path) + ".md5").read_text().strip()
         got = _ext.native().md5_file(str(path))
@@ -109,20 +109,41 @@ def load_ckpt_vanilla(model, optimizer, lr_scheduler=None, sampler=None, checkpo
         checkpoint_path = core.get_latest_checkpoint(str(experiment_dir))
         if checkpoint_path is None:
             raise RuntimeError(f"No checkpoint found in {experiment_dir}")
-    result = {"ok": True, "err": ""}
-    th = None
-    if verify and rank == 0:
-        def _v():
-            result["ok"], result["err"] = verify_checkpoint(checkpoint_path)
-        th = threading.Thread(target=_v, daemon=True)
-        th.start()
-    ckpt = torch.load(checkpoint_path, map_location="cpu", mmap=True, weights_only=True)
-    epoch, step = load_state_into(model, optimizer, lr_scheduler, sampler, ckpt)
-    del ckpt
-    if th is not None:
-        th.join()
-        if not result["ok"]:
-            raise RuntimeError(result["err"])
+    from . import fastload
+
+    plan = None
+    if fastload.ENABLED:
+        try:
+            plan = fastload.plan_vanilla(str(checkpoint_path), model, optimizer)
+        except (ValueError, KeyError, OSError, RuntimeError) as e:  # not an archive the planner maps
+            logger.info(f"fast load not applicable ({e}); using torch.load")
+    if plan is not None:
+        # native parallel read straight into the flat buffers, .md5parts verified on the way
+        ckpt, pl = plan
+        md5parts = fastload.read_md5parts(str(checkpoint_path)) if verify else None
+        if md5parts is not None and md5parts[1] != Path(checkpoint_path).stat().st_size:
+            raise RuntimeError(f"Checksum mismatch for checkpoint {checkpoint_path}: size differs from its md5parts")
+        stats = fastload.execute(pl, fastload.flat_buffers(model, optimizer), verify, md5parts,
+                                 str(checkpoint_path), is_distributed)
+        epoch, step = fastload.finish_state(model, optimizer, lr_scheduler, sampler, ckpt, pl)
+        del ckpt
+        logger.info(f"native read: {stats['bytes_read'] / 2**30:.2f} GiB in {stats['read_s']:.2f}s "
+                    f"(verified: {stats['verified']})")
+    else:
+        result = {"ok": True, "err": ""}
+        th = None
+        if verify and rank == 0:
+            def _v():
+                result["ok"], result["err"] = verify_checkpoint(checkpoint_path)
+            th = threading.Thread(target=_v, daemon=True)
+            th.start()
+        ckpt = torch.load(checkpoint_path, map_location="cpu", mmap=True, weights_only=True)
+        epoch, step = load_state_into(model, optimizer, lr_scheduler, sampler, ckpt)
+        del ckpt
+        if th is not None:
+            th.join()
+            if not result["ok"]:
+                raise RuntimeError(result["err"])
     if is_distributed:
         dist.barrier()
     logger.info(f"Checkpoint loaded from {checkpoint_path} (epoch {epoch}, step {step})")

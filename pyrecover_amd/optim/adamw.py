@@ -198,8 +198,10 @@ class FlatAdamW(torch.optim.AdamW):
             st["step"] = torch.tensor(float(self._step), dtype=torch.float32)
         return super().state_dict()
 
-    def load_state_dict(self, state_dict):
-        """Accepts torch.optim.AdamW state dicts (ours or the reference's)."""
+    def load_state_dict(self, state_dict, tensors_loaded: bool = False):
+        """Accepts torch.optim.AdamW state dicts (ours or the reference's). ``tensors_loaded``:
+        the moments were already written into the flat buffers (native resume path), so only the
+        hyper-parameters and step counts are taken from ``state_dict``."""
         groups = state_dict["param_groups"]
         if len(groups) != 1:
             raise ValueError("expected exactly one param group")
@@ -216,11 +218,13 @@ class FlatAdamW(torch.optim.AdamW):
                 st = state_dict["state"].get(sid, state_dict["state"].get(str(sid)))
                 mine = self.state[p]
                 if st is None:
-                    mine["exp_avg"].zero_()
-                    mine["exp_avg_sq"].zero_()
+                    if not tensors_loaded:
+                        mine["exp_avg"].zero_()
+                        mine["exp_avg_sq"].zero_()
                     continue
-                mine["exp_avg"].copy_(st["exp_avg"])
-                mine["exp_avg_sq"].copy_(st["exp_avg_sq"])
+                if not tensors_loaded:
+                    mine["exp_avg"].copy_(st["exp_avg"])
+                    mine["exp_avg_sq"].copy_(st["exp_avg_sq"])
                 steps.add(float(st["step"]))
         if len(steps) > 1:
             raise ValueError(f"inconsistent per-parameter step counts {sorted(steps)}")

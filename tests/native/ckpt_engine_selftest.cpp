@@ -1,8 +1,9 @@
 // Standalone self-test of the checkpoint engine core (csrc/runtime/ckpt_engine.h) in CPU mode
 // (device -1: no HIP calls), built with -fsanitize=address,undefined or -fsanitize=thread by
 // tests/test_native_sanitizers.py. Exercises: pool reserve, parallel host staging, the writer
-// thread (zip records + raw blob in one file, CRC32 pieces, pipelined MD5, tmp+rename, .md5
-// sidecar), the error path, and back-to-back jobs reusing the pool.
+// threads (zip records + raw blob in one file, CRC32 pieces, parallel segment writes + MD5s,
+// whole-file MD5, tmp+rename, .md5 sidecar), the parallel Reader (O_DIRECT and buffered), the
+// error paths, and back-to-back jobs reusing the pool.
 // usage: ckpt_engine_selftest <out_dir>   -> exit 0 on success; writes <out_dir>/t.bin
 #include "runtime/ckpt_engine.h"
 
@@ -70,6 +71,26 @@ int main(int argc, char** argv) {
     REQUIRE(md5_file(path) == r.md5);
     REQUIRE(slurp(path + ".md5") == r.md5);
     REQUIRE(access((path + ".tmp").c_str(), F_OK) != 0);
+    REQUIRE(r.seg_md5.size() == (r.bytes + kSegBytes - 1) / kSegBytes);
+    // every zip record's payload sits at the reported offset
+    REQUIRE(r.records.size() == 3);
+    for (size_t i = 0; i < src.size(); ++i)
+      REQUIRE(std::memcmp(file.data() + r.records[i].data_off, src[i].data(), src[i].size()) == 0);
+    // parallel reader (CPU mode, several threads): payloads back into fresh buffers, segment hash
+    std::vector<std::vector<uint8_t>> back(src.size());
+    std::vector<ReadItem> ri;
+    for (size_t i = 0; i < src.size(); ++i) {
+      back[i].assign(src[i].size(), 0);
+      ri.push_back({r.records[i].data_off, src[i].size(), (uintptr_t)back[i].data()});
+    }
+    Reader rd(-1);
+    const ReadResult rr = rd.read(path, ri, {0}, 4, /*direct=*/round == 0);
+    REQUIRE(rr.ok);
+    REQUIRE(rr.seg_md5.size() == r.seg_md5.size() && rr.seg_md5[0] == r.seg_md5[0]);
+    for (size_t i = 0; i < src.size(); ++i) REQUIRE(back[i] == src[i]);
+    // an item past the end of the file is an error, not a fault
+    const ReadResult bad_rd = rd.read(path, {{r.bytes - 4, 64, (uintptr_t)back[0].data()}}, {}, 2, false);
+    REQUIRE(!bad_rd.ok && !bad_rd.error.empty());
   }
   // error path: unwritable destination -> ok=false, message, nothing left behind
   eng.write_items(dir + "/no/such/dir/x.bin", {}, true, false);
