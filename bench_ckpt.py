@@ -127,9 +127,10 @@ def main():
 
     if "async" in formats:
         p = os.path.join(args.dir, "ckpt_3.pt")
-        # as train.py --async-checkpoint does: the pinned pool is allocated in the background
-        # while training runs, so the first save does not pay for it
-        core.Checkpointer.get(flat.data.device).prewarm(int(3 * flat.state_bytes() * 1.05) + (64 << 20))
+        # as train.py --async-checkpoint does: the pinned pool is allocated before training runs,
+        # so the first save does not pay for it
+        core.Checkpointer.get(flat.data.device).prewarm(int(3 * flat.state_bytes() * 1.05) + (64 << 20),
+                                                        background=False)
         step()
         step()
         torch.cuda.synchronize()

@@ -144,10 +144,15 @@ class Checkpointer:
         self.staged = False
         self._prewarm: Optional[threading.Thread] = None
 
-    def prewarm(self, nbytes: int):
-        """Allocate the pinned staging pool in the background (hipHostMalloc of tens of GB takes
-        seconds), so the first async checkpoint does not stall training on it."""
+    def prewarm(self, nbytes: int, background: bool = True):
+        """Allocate the pinned staging pool ahead of the first checkpoint. Prefer
+        ``background=False`` before training starts: hipHostMalloc updates the GPU page tables,
+        which serializes behind running kernels (a background allocation overlapping the first
+        training steps stalled them for minutes on MI355X), while on an idle GPU it takes ~0.2 s/GB."""
         if self._prewarm is not None or nbytes <= self.engine.pool_size():
+            return
+        if not background:
+            self.engine.reserve(int(nbytes))
             return
         self._prewarm = threading.Thread(target=self.engine.reserve, args=(int(nbytes),), daemon=True,
                                          name="pyrecover-ckpt-prewarm")
