@@ -564,7 +564,8 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const T* __restrict__
 }
 
 // ======================================================================================
-// Backward preprocess: delta[b,h,q] = sum_d dO[q,h,d] * O[q,h,d]  (fp32)
+// Backward preprocess (PRA_ATTN_DELTA_PRE=1 only; by default the dQ kernel computes delta itself):
+// delta[b,h,q] = sum_d dO[q,h,d] * O[q,h,d]  (fp32)
 // Block = (b, PRE_QB consecutive queries, all heads): the [PRE_QB, Hq, D] slabs of O and dO are
 // contiguous per token, so the reads stream at full width with 4 rows in flight per lane; the
 // per-row sums are staged in LDS and written out along q (runs of PRE_QB floats per head) instead
@@ -959,9 +960,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
 template <typename T, int D, bool CAUSAL, int NW, bool PIPE = false>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
     const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V,
-    const T* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
-    T* __restrict__ dQ, int S, int Hq, int Hkv, long ldq, long ldk, long ldv, long lddo, long lddq,
-    float scale, float scale_log2, int prio, int skv) {
+    const T* __restrict__ dO, const T* __restrict__ O, const float* __restrict__ LSE, float* __restrict__ Delta,
+    T* __restrict__ dQ, int S, int Hq, int Hkv, long ldq, long ldk, long ldv, long lddo, long ldo, long lddq,
+    float scale, float scale_log2, int prio, int skv, int delta_in) {
   constexpr int KT = 64, QT = 32 * NW;
   constexpr int NKS = D / 16, NDB = D / 32, TILE = KT * D;
   __shared__ __attribute__((aligned(16))) T smem[4 * TILE];  // K0 V0 K1 V1
@@ -996,10 +997,28 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
       }
     }
   }
+  // delta = rowsum(dO * O) of this lane's query row, computed here (this kernel runs before the
+  // dK/dV kernel and publishes it; no separate preprocess pass): the lane holds half of the dO row
+  // (columns 16 ks + 8 h2 ..), its partner lane l ^ 32 the other half.
   float lse2 = 0.f, dl = 0.f;
-  if (qrow < S) {
-    lse2 = LSE[((long)b * Hq + hq) * S + qrow] * 1.4426950408889634f;
-    dl = Delta[((long)b * Hq + hq) * S + qrow];
+  {
+    float part = 0.f;
+    if (qrow < S) lse2 = LSE[((long)b * Hq + hq) * S + qrow] * 1.4426950408889634f;
+    if (delta_in) {
+      if (qrow < S) dl = Delta[((long)b * Hq + hq) * S + qrow];
+    } else {
+    if (qrow < S) {
+      const T* Orow = O + ((long)b * S + qrow) * ldo + hq * D + 8 * h2;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const V8<T> o8 = *reinterpret_cast<const V8<T>*>(Orow + 16 * ks);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) part = fmaf((float)o8[j], (float)df[ks][j], part);
+      }
+    }
+    dl = half_sum(part);  // all 64 lanes (permlane32 swap)
+    if (qrow < S && h2 == 0) Delta[((long)b * Hq + hq) * S + qrow] = dl;
+    }
   }
 
   f32x16 dqt[NDB];
@@ -1186,15 +1205,47 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
     const char* e = getenv("PRA_ATTN_BWD_PRIO");
     return e ? atoi(e) : 0;
   }();
-  {
+  // dQ first: it also computes delta = rowsum(dO * O), which the dK/dV kernel reads
+  // (PRA_ATTN_DELTA_PRE=1: a separate preprocess kernel computes it, read per call for A/B tests)
+  const char* dpre_s = getenv("PRA_ATTN_DELTA_PRE");
+  const int delta_pre = dpre_s ? atoi(dpre_s) : 0;
+  if (delta_pre) {
     if (Hq > PRE_MAXH) return hipErrorInvalidValue;
     const int grid = B * (S / PRE_QB);
     if (D == 128)
-      hipLaunchKernelGGL((bwd_pre_kernel<T, 128>), dim3(grid), dim3(256), 0, st, (const T*)o,
-                         (const T*)dout, delta, B, S, Hq, ldo, lddo);
+      hipLaunchKernelGGL((bwd_pre_kernel<T, 128>), dim3(grid), dim3(256), 0, st, (const T*)o, (const T*)dout, delta, B,
+                         S, Hq, ldo, lddo);
     else
-      hipLaunchKernelGGL((bwd_pre_kernel<T, 64>), dim3(grid), dim3(256), 0, st, (const T*)o,
-                         (const T*)dout, delta, B, S, Hq, ldo, lddo);
+      hipLaunchKernelGGL((bwd_pre_kernel<T, 64>), dim3(grid), dim3(256), 0, st, (const T*)o, (const T*)dout, delta, B,
+                         S, Hq, ldo, lddo);
+  }
+  {
+    static const int dq_env = [] {
+      const char* e = getenv("PRA_DQ_NW");
+      return e ? atoi(e) : 0;
+    }();
+    const int nwq = (dq_env == 4 || S % 256) ? 4 : 8;
+    dim3 grid(((S + 32 * nwq - 1) / (32 * nwq)) * Hq * B);
+    const char* pipe_s = getenv("PRA_DQ_PIPE");  // read per call (tests switch it)
+    // the pipelined kernel has no key bound: padded non-causal sequences take the plain one
+    const bool pipe = (causal || skv >= S) && (pipe_s ? atoi(pipe_s) != 0 : true);
+#define LAUNCH(DD, CC, NWW)                                                                                     \
+  if (pipe)                                                                                                     \
+  hipLaunchKernelGGL((bwd_dq_kernel<T, DD, CC, NWW, true>), grid, dim3(NWW * 64), 0, st, (const T*)q,         \
+                     (const T*)k, (const T*)v, (const T*)dout, (const T*)o, lse, delta, (T*)dq, S, \
+                     Hq, Hkv, ldq, ldk, ldv, lddo, ldo, lddq, scale, sl2, bwd_prio, skv, delta_pre);                                            \
+  else                                                                                                          \
+  hipLaunchKernelGGL((bwd_dq_kernel<T, DD, CC, NWW>), grid, dim3(NWW * 64), 0, st, (const T*)q,               \
+                     (const T*)k, (const T*)v, (const T*)dout, (const T*)o, lse, delta, (T*)dq, S, \
+                     Hq, Hkv, ldq, ldk, ldv, lddo, ldo, lddq, scale, sl2, bwd_prio, skv, delta_pre)
+    if (nwq == 8) {
+      if (D == 128) { if (causal) LAUNCH(128, true, 8); else LAUNCH(128, false, 8); }
+      else { if (causal) LAUNCH(64, true, 8); else LAUNCH(64, false, 8); }
+    } else {
+      if (D == 128) { if (causal) LAUNCH(128, true, 4); else LAUNCH(128, false, 4); }
+      else { if (causal) LAUNCH(64, true, 4); else LAUNCH(64, false, 4); }
+    }
+#undef LAUNCH
   }
   {
     static const int nw_env = [] {
@@ -1234,34 +1285,6 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
     }
 #undef LAUNCH
     }
-  }
-  {
-    static const int dq_env = [] {
-      const char* e = getenv("PRA_DQ_NW");
-      return e ? atoi(e) : 0;
-    }();
-    const int nwq = (dq_env == 4 || S % 256) ? 4 : 8;
-    dim3 grid(((S + 32 * nwq - 1) / (32 * nwq)) * Hq * B);
-    const char* pipe_s = getenv("PRA_DQ_PIPE");  // read per call (tests switch it)
-    // the pipelined kernel has no key bound: padded non-causal sequences take the plain one
-    const bool pipe = (causal || skv >= S) && (pipe_s ? atoi(pipe_s) != 0 : true);
-#define LAUNCH(DD, CC, NWW)                                                                                     \
-  if (pipe)                                                                                                     \
-  hipLaunchKernelGGL((bwd_dq_kernel<T, DD, CC, NWW, true>), grid, dim3(NWW * 64), 0, st, (const T*)q,         \
-                     (const T*)k, (const T*)v, (const T*)dout, lse, delta, (T*)dq, S, Hq, Hkv,  \
-                     ldq, ldk, ldv, lddo, lddq, scale, sl2, bwd_prio, skv);                                            \
-  else                                                                                                          \
-  hipLaunchKernelGGL((bwd_dq_kernel<T, DD, CC, NWW>), grid, dim3(NWW * 64), 0, st, (const T*)q,               \
-                     (const T*)k, (const T*)v, (const T*)dout, lse, delta, (T*)dq, S, Hq, Hkv,  \
-                     ldq, ldk, ldv, lddo, lddq, scale, sl2, bwd_prio, skv)
-    if (nwq == 8) {
-      if (D == 128) { if (causal) LAUNCH(128, true, 8); else LAUNCH(128, false, 8); }
-      else { if (causal) LAUNCH(64, true, 8); else LAUNCH(64, false, 8); }
-    } else {
-      if (D == 128) { if (causal) LAUNCH(128, true, 4); else LAUNCH(128, false, 4); }
-      else { if (causal) LAUNCH(64, true, 4); else LAUNCH(64, false, 4); }
-    }
-#undef LAUNCH
   }
   return hipGetLastError();
 }
