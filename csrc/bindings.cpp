@@ -405,6 +405,44 @@ void adamw_flat_(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, 
         "adamw_flat");
 }
 
+// AdamW of one row-major weight matrix p [rows, cols] that also writes pt = p^T [cols, rows].
+void adamw_t_(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, at::Tensor pt, double lr, double b1,
+              double b2, double eps, double wd, double bc1, double bc2_sqrt, double gscale,
+              const c10::optional<at::Tensor>& gscale_dev, const c10::optional<at::Tensor>& hyper_dev) {
+  const Range range_("pyrecover::adamw_t");
+  check_dev(p, "p");
+  TORCH_CHECK(p.dim() == 2 && p.is_contiguous() && g.sizes() == p.sizes() && m.sizes() == p.sizes() &&
+                  v.sizes() == p.sizes() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous(),
+              "adamw_t: p/g/m/v must be contiguous [rows, cols]");
+  const int64_t rows = p.size(0), cols = p.size(1);
+  TORCH_CHECK(pt.dim() == 2 && pt.size(0) == cols && pt.size(1) == rows && pt.is_contiguous(), "adamw_t: pt [cols, rows]");
+  TORCH_CHECK(rows % 64 == 0 && cols % 64 == 0, "adamw_t: rows and cols must be multiples of 64");
+  TORCH_CHECK(p.element_size() == 2, "adamw_t: 16-bit parameters required");
+  for (const at::Tensor& t : {g, m, v, pt}) {
+    same_dev(p, t, "adamw_t operand");
+    TORCH_CHECK(t.scalar_type() == p.scalar_type(), "adamw_t: dtypes must match");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "adamw_t: operands must be 16-B aligned");
+  }
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(p.data_ptr()) % 16 == 0, "adamw_t: p must be 16-B aligned");
+  const c10::DeviceGuard guard(p.device());
+  const float* gsd = nullptr;
+  if (gscale_dev.has_value()) {
+    TORCH_CHECK(gscale_dev->scalar_type() == at::kFloat && gscale_dev->numel() >= 1, "adamw_t: gscale_dev fp32");
+    same_dev(p, *gscale_dev, "gscale_dev");
+    gsd = gscale_dev->data_ptr<float>();
+  }
+  const float* hyd = nullptr;
+  if (hyper_dev.has_value()) {
+    TORCH_CHECK(hyper_dev->scalar_type() == at::kFloat && hyper_dev->numel() >= 3, "adamw_t: hyper_dev fp32[3]");
+    same_dev(p, *hyper_dev, "hyper_dev");
+    hyd = hyper_dev->data_ptr<float>();
+  }
+  check(pra_adamw_t(dt(p), p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), pt.data_ptr(), (int)rows,
+                    (int)cols, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1, (float)bc2_sqrt,
+                    (float)gscale, gsd, hyd, stream_of(p)),
+        "adamw_t");
+}
+
 // dst = src^T for a 2-D 16-bit tensor (bf16/fp16) with R, C multiples of 64 (dst: optional
 // preallocated [C, R] row-major output).
 at::Tensor transpose2d(const at::Tensor& src, c10::optional<at::Tensor> out) {
@@ -582,6 +620,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("xent_bwd_", &xent_bwd_);
   namespace py = pybind11;
   m.def("adamw_flat_", &adamw_flat_, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("lr"),
+        py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("bc1"), py::arg("bc2_sqrt"),
+        py::arg("gscale"), py::arg("gscale_dev") = py::none(), py::arg("hyper_dev") = py::none());
+  m.def("adamw_t_", &adamw_t_, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("pt"), py::arg("lr"),
         py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("bc1"), py::arg("bc2_sqrt"),
         py::arg("gscale"), py::arg("gscale_dev") = py::none(), py::arg("hyper_dev") = py::none());
   m.def("grad_norm", &grad_norm);

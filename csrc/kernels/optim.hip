@@ -18,6 +18,18 @@
 
 namespace pra {
 
+// One AdamW element update with every fused multiply-add written out, so all kernels that use it
+// (flat, tiled + transposed) round identically whatever the compiler's contraction choices.
+__device__ __forceinline__ void adamw_elem(float& p, float& m, float& v, float g, float gs, float decay, float b1,
+                                           float b2, float eps, float bc2_sqrt, float step_size) {
+  const float gr = g * gs;
+  p *= decay;
+  m = fmaf(1.f - b1, gr - m, m);
+  v = fmaf(b2, v, (1.f - b2) * (gr * gr));
+  const float denom = __fdiv_rn(sqrtf(v), bc2_sqrt) + eps;
+  p = fmaf(-step_size, __fdiv_rn(m, denom), p);
+}
+
 template <typename P, typename S>
 __global__ __launch_bounds__(256) void adamw_kernel(P* __restrict__ p, const P* __restrict__ g, S* __restrict__ m,
                                                     S* __restrict__ v, long n, float lr, float b1, float b2,
@@ -41,28 +53,68 @@ __global__ __launch_bounds__(256) void adamw_kernel(P* __restrict__ p, const P* 
     load8<S>(m + o, mv);
     load8<S>(v + o, vv);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float gr = gv[j] * gs;
-      pv[j] *= decay;
-      mv[j] = mv[j] + (1.f - b1) * (gr - mv[j]);
-      vv[j] = b2 * vv[j] + (1.f - b2) * gr * gr;
-      const float denom = sqrtf(vv[j]) / bc2_sqrt + eps;
-      pv[j] = pv[j] - step_size * mv[j] / denom;
-    }
+    for (int j = 0; j < 8; ++j) adamw_elem(pv[j], mv[j], vv[j], gv[j], gs, decay, b1, b2, eps, bc2_sqrt, step_size);
     store8<P>(p + o, pv);
     store8<S>(m + o, mv);
     store8<S>(v + o, vv);
   }
   // tail
   for (long o = n8 * 8 + (long)blockIdx.x * 256 + threadIdx.x; o < n; o += (long)gridDim.x * 256) {
-    float pv = to_f<P>(p[o]), gr = to_f<P>(g[o]) * gs, mv = to_f<S>(m[o]), vv = to_f<S>(v[o]);
-    pv *= decay;
-    mv = mv + (1.f - b1) * (gr - mv);
-    vv = b2 * vv + (1.f - b2) * gr * gr;
-    pv = pv - step_size * mv / (sqrtf(vv) / bc2_sqrt + eps);
+    float pv = to_f<P>(p[o]), mv = to_f<S>(m[o]), vv = to_f<S>(v[o]);
+    adamw_elem(pv, mv, vv, to_f<P>(g[o]), gs, decay, b1, b2, eps, bc2_sqrt, step_size);
     p[o] = from_f<P>(pv);
     m[o] = from_f<S>(mv);
     v[o] = from_f<S>(vv);
+  }
+}
+
+// AdamW over one row-major [rows, cols] weight matrix that ALSO writes its transposed copy
+// pt [cols, rows] (the data-gradient GEMM's operand, parallel/flat.py "weight shadows") from the
+// updated values it already holds: the separate transpose pass re-read the whole model after
+// every update (13.5 GB/step at 7B). Block = one 64 x 64 tile; the updated p tile goes through
+// LDS (padded rows) to 16-B transposed stores. Same math and rounding as adamw_kernel.
+template <typename P>
+__global__ __launch_bounds__(256) void adamw_t_kernel(P* __restrict__ p, const P* __restrict__ g, P* __restrict__ m,
+                                                      P* __restrict__ v, P* __restrict__ pt, int rows, int cols,
+                                                      float lr, float b1, float b2, float eps, float wd, float bc1,
+                                                      float bc2_sqrt, float gscale, const float* __restrict__ gscale_dev,
+                                                      const float* __restrict__ hyper_dev) {
+  __shared__ uint16_t tile[64][72];
+  const float gs = gscale_dev ? gscale * gscale_dev[0] : gscale;
+  if (hyper_dev) {
+    lr = hyper_dev[0];
+    bc1 = hyper_dev[1];
+    bc2_sqrt = hyper_dev[2];
+  }
+  const float decay = 1.f - lr * wd;
+  const float step_size = lr / bc1;
+  const long r0 = (long)blockIdx.y * 64, c0 = (long)blockIdx.x * 64;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int idx = threadIdx.x + 256 * k, r = idx >> 3, ch = idx & 7;
+    const long o = (r0 + r) * cols + c0 + 8 * ch;
+    float pv[8], gv[8], mv[8], vv[8];
+    load8<P>(p + o, pv);
+    load8<P>(g + o, gv);
+    load8<P>(m + o, mv);
+    load8<P>(v + o, vv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) adamw_elem(pv[j], mv[j], vv[j], gv[j], gs, decay, b1, b2, eps, bc2_sqrt, step_size);
+    store8<P>(p + o, pv);
+    store8<P>(m + o, mv);
+    store8<P>(v + o, vv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tile[r][8 * ch + j] = __builtin_bit_cast(uint16_t, from_f<P>(pv[j]));
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int idx = threadIdx.x + 256 * k, c = idx >> 3, rg = idx & 7;
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      w[j] = (uint32_t)tile[8 * rg + 2 * j][c] | ((uint32_t)tile[8 * rg + 2 * j + 1][c] << 16);
+    *reinterpret_cast<uint4*>(pt + (c0 + c) * rows + r0 + 8 * rg) = make_uint4(w[0], w[1], w[2], w[3]);
   }
 }
 
@@ -116,6 +168,20 @@ hipError_t pra_adamw_flat(int pdtype, int sdtype, void* p, const void* g, void* 
                      hipLaunchKernelGGL((pra::adamw_kernel<T, T>), dim3(blocks), dim3(256), 0, s, (T*)p, (const T*)g,
                                         (T*)m, (T*)v, n, lr, b1, b2, eps, wd, bc1, bc2_sqrt, gscale, gscale_dev,
                                         hyper_dev));
+  return hipGetLastError();
+}
+
+// AdamW of one [rows, cols] matrix + its transposed copy pt [cols, rows] (rows, cols % 64 == 0;
+// 16-bit params, moments of the same dtype).
+hipError_t pra_adamw_t(int dtype, void* p, const void* g, void* m, void* v, void* pt, int rows, int cols, float lr,
+                       float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt, float gscale,
+                       const float* gscale_dev, const float* hyper_dev, hipStream_t s) {
+  if (rows % 64 || cols % 64 || rows <= 0 || cols <= 0) return hipErrorInvalidValue;
+  const dim3 grid(cols / 64, rows / 64);
+  PRA_DISPATCH_16BIT(dtype, T,
+                     hipLaunchKernelGGL((pra::adamw_t_kernel<T>), grid, dim3(256), 0, s, (T*)p, (const T*)g, (T*)m,
+                                        (T*)v, (T*)pt, rows, cols, lr, b1, b2, eps, wd, bc1, bc2_sqrt, gscale,
+                                        gscale_dev, hyper_dev));
   return hipGetLastError();
 }
 

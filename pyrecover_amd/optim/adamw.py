@@ -10,12 +10,18 @@ over the whole model (``pra_adamw_flat``: fp32 opmath, torch ``_fused_adamw_`` s
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
 
 from .. import _ext
 from ..parallel.flat import FlatParams
+
+# Matrices with a transposed weight shadow (parallel/flat.py) are updated by a tiled AdamW kernel
+# that writes the shadow from the values it just computed (no transpose pass re-reading the
+# weights); PRA_FUSED_ADAMW_T=0 falls back to flat AdamW + a separate transpose.
+FUSED_T = os.environ.get("PRA_FUSED_ADAMW_T", "1") == "1"
 
 
 class FlatAdamW(torch.optim.AdamW):
@@ -90,16 +96,38 @@ class FlatAdamW(torch.optim.AdamW):
         lr, eps, wd = float(g["lr"]), float(g["eps"]), float(g["weight_decay"])
         return lr, b1, b2, eps, wd, 1.0 - b1 ** self._step, math.sqrt(1.0 - b2 ** self._step)
 
-    def _update_range(self, lo, hi):
+    def _update_range(self, lo, hi, coeffs=None):
         f = self.flat
-        lr, b1, b2, eps, wd, bc1, bc2_sqrt = self._coeffs()
-        if _ext.hip(f.data):
-            _ext.require_for(f.data).adamw_flat_(f.data[lo:hi], f.grad[lo:hi], self.exp_avg[lo:hi],
-                                                 self.exp_avg_sq[lo:hi], lr, b1, b2, eps, wd, bc1, bc2_sqrt,
-                                                 self.grad_scale, self.grad_scale_dev, self.hyper)
-            f.refresh_transposed(lo, hi)  # same stream: the next backward sees the new weights
-        else:
+        lr, b1, b2, eps, wd, bc1, bc2_sqrt = coeffs if coeffs is not None else self._coeffs()
+        if not _ext.hip(f.data):
             self._step_reference(lr, b1, b2, eps, wd, bc1, bc2_sqrt, lo, hi)
+            return
+        C = _ext.require_for(f.data)
+        args = (lr, b1, b2, eps, wd, bc1, bc2_sqrt, self.grad_scale, self.grad_scale_dev, self.hyper)
+        m, v = self.exp_avg, self.exp_avg_sq
+
+        def flat_update(a, b):
+            if a < b:
+                C.adamw_flat_(f.data[a:b], f.grad[a:b], m[a:b], v[a:b], *args)
+
+        mats = f.transposed_in(lo, hi) if FUSED_T else []
+        cur = lo
+        rest = []
+        for o, rows, cols in mats:
+            n = rows * cols
+            if o + n > hi:  # (buckets align to fusion groups; kept for safety)
+                rest.append(o)
+                continue
+            flat_update(cur, o)
+            sl = slice(o, o + n)
+            C.adamw_t_(f.data[sl].view(rows, cols), f.grad[sl].view(rows, cols), m[sl].view(rows, cols),
+                       v[sl].view(rows, cols), f.data_t[sl].view(cols, rows), *args)
+            cur = o + n
+        flat_update(cur, hi)
+        if not FUSED_T:
+            f.refresh_transposed(lo, hi)  # same stream: the next backward sees the new weights
+        for o in rest:
+            f.refresh_transposed(o, o + 1)
 
     def _on_bucket(self, b, lo, hi, work):
         if not self.overlap or self.grad_scale_dev is not None:
@@ -164,13 +192,7 @@ class FlatAdamW(torch.optim.AdamW):
         lr, eps, wd = float(g["lr"]), float(g["eps"]), float(g["weight_decay"])
         bc1 = 1.0 - b1 ** self._step
         bc2_sqrt = math.sqrt(1.0 - b2 ** self._step)
-        f = self.flat
-        if _ext.hip(f.data):
-            _ext.require_for(f.data).adamw_flat_(f.data, f.grad, self.exp_avg, self.exp_avg_sq, lr, b1, b2, eps, wd,
-                                                 bc1, bc2_sqrt, self.grad_scale, self.grad_scale_dev, self.hyper)
-            f.refresh_transposed()
-        else:
-            self._step_reference(lr, b1, b2, eps, wd, bc1, bc2_sqrt)
+        self._update_range(0, self.flat.numel, (lr, b1, b2, eps, wd, bc1, bc2_sqrt))
         return loss
 
     def _step_reference(self, lr, b1, b2, eps, wd, bc1, bc2_sqrt, lo=0, hi=None):

@@ -164,6 +164,15 @@ class FlatParams:
         _, rows, cols = self.t_mats[i]
         return self.data_t[o:o + rows * cols].view(cols, rows)
 
+    def transposed_in(self, lo: int, hi: int) -> List[Tuple[int, int, int]]:
+        """(offset, rows, cols) of the registered matrices starting inside [lo, hi), in offset
+        order; the transposed buffer exists afterwards (an optimizer writing the shadows itself)."""
+        if not getattr(self, "t_mats", None):
+            return []
+        if self.data_t is None:
+            self.refresh_transposed()
+        return [m for m in self.t_mats if lo <= m[0] < hi]
+
     def refresh_transposed(self, lo: int = 0, hi: Optional[int] = None):
         """Re-derive the transposed copies of registered matrices inside [lo, hi), on the current
         stream (call after anything that writes parameters)."""

@@ -341,3 +341,28 @@ def test_rope_t_matches_rope_exactly(cuda):
     xT = C_.rope_t_(x2, (Hq + Hkv) * D, tab, D, S, True)
     assert torch.equal(x2, ref)
     assert torch.equal(xT, ref.t().contiguous())
+
+
+@pytest.mark.parametrize("rows,cols", [(64, 64), (192, 320), (4096, 128)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_adamw_t_matches_flat_adamw_plus_transpose(cuda, rows, cols, dtype):
+    """Fused AdamW + transposed-shadow write == flat AdamW followed by transpose2d, bit for bit
+    (incl. device-side grad scale and hyper-parameters)."""
+    C = _ext.native()
+    torch.manual_seed(rows + cols)
+    p = torch.randn(rows, cols, device=cuda).to(dtype)
+    g = (torch.randn(rows, cols, device=cuda) * 1e-2).to(dtype)
+    m = (torch.randn(rows, cols, device=cuda) * 1e-3).to(dtype)
+    v = (torch.rand(rows, cols, device=cuda) * 1e-4).to(dtype)
+    gs = torch.tensor([0.7], device=cuda)
+    hy = torch.tensor([3e-4, 0.19, 0.031], device=cuda)
+    a = [t.clone() for t in (p, g, m, v)]
+    C.adamw_flat_(a[0].view(-1), a[1].view(-1), a[2].view(-1), a[3].view(-1), 1e-3, 0.9, 0.95, 1e-8, 0.1, 0.5, 0.2,
+                  0.5, gs, hy)
+    pt_ref = C.transpose2d(a[0])
+    b = [t.clone() for t in (p, g, m, v)]
+    pt = torch.empty(cols, rows, device=cuda, dtype=dtype)
+    C.adamw_t_(b[0], b[1], b[2], b[3], pt, 1e-3, 0.9, 0.95, 1e-8, 0.1, 0.5, 0.2, 0.5, gs, hy)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    assert torch.equal(pt, pt_ref)
