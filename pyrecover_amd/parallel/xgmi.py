@@ -14,8 +14,10 @@ Per bucket, the traffic per link is bucket/W per phase.
 
 Cross-process ordering uses interprocess HIP events only. A peer's copy stream waits, on the GPU,
 on this rank's "bucket ready" / "slice reduced" events, and no kernel spins. The host only
-guarantees that an event was recorded before anyone waits on it. A dedicated comm thread does this
-with two CPU (gloo) barriers per bucket, so the backward thread never blocks.
+guarantees that an event was recorded (for THIS step) before anyone waits on it: every rank
+publishes a per-bucket sequence number in a page of host shared memory right after recording, and
+the comm thread of a peer polls that word (microseconds) instead of the two gloo barriers per
+bucket an earlier version paid (a TCP round trip each). The backward thread never blocks.
 
 The gradient buffer is reallocated with ``hipMalloc`` so it can be exported with
 ``hipIpcGetMemHandle``. Opt-in: ``GradReducer(..., backend="xgmi")``, ``train.py --allreduce
@@ -25,7 +27,12 @@ from __future__ import annotations
 
 import queue
 import threading
+import time
+import uuid
+from multiprocessing import shared_memory
 from typing import List, Sequence, Tuple
+
+import numpy as np
 
 import torch
 import torch.distributed as dist
@@ -47,6 +54,63 @@ class _Work:
         if self.owner.error is not None:
             raise RuntimeError(f"xgmi all-reduce failed: {self.owner.error}")
         torch.cuda.current_stream(self.owner.dev).wait_event(self.owner.ev_done[self.b])
+
+
+class _HostSeq:
+    """[world, slots] int64 sequence words in one POSIX shared-memory page set (node-local ranks):
+    rank r publishes ``seq`` in its own row; readers poll a peer's word until it reaches ``seq``.
+    Aligned 8-byte stores/loads are single-copy atomic on x86-64."""
+
+    def __init__(self, rank: int, world: int, slots: int, group):
+        name = [f"pra_xgmi_{uuid.uuid4().hex[:16]}" if rank == 0 else None]
+        dist.broadcast_object_list(name, src=0, group=group)
+        size = world * slots * 8
+        self.owner = rank == 0
+        if self.owner:
+            self.shm = shared_memory.SharedMemory(name=name[0], create=True, size=size)
+        dist.barrier(group=group)
+        if not self.owner:
+            self.shm = shared_memory.SharedMemory(name=name[0], create=False, size=size)
+            # Python < 3.13 registers attached segments with the resource tracker too, which would
+            # unlink rank 0's segment when this process exits; only the creator owns it
+            from multiprocessing import resource_tracker
+
+            resource_tracker.unregister(self.shm._name, "shared_memory")
+        else:
+            import atexit
+
+            atexit.register(self.close)  # never leave the page behind in /dev/shm
+        self.a = np.ndarray((world, slots), dtype=np.int64, buffer=self.shm.buf)
+        if self.owner:
+            self.a[:] = 0
+        dist.barrier(group=group)
+        self.rank = rank
+
+    def publish(self, slot: int, seq: int):
+        self.a[self.rank, slot] = seq
+
+    def wait(self, r: int, slot: int, seq: int, timeout: float = 600.0):
+        if self.a[r, slot] >= seq:
+            return
+        t0 = time.perf_counter()
+        spins = 0
+        while self.a[r, slot] < seq:
+            spins += 1
+            if spins > 200:
+                time.sleep(20e-6)  # releases the GIL for the backward thread
+            if time.perf_counter() - t0 > timeout:
+                raise TimeoutError(f"xgmi: rank {r} did not publish slot {slot} seq {seq}")
+
+    def close(self):
+        if getattr(self, "a", None) is None:
+            return
+        self.a = None
+        self.shm.close()
+        if self.owner:
+            try:
+                self.shm.unlink()
+            except FileNotFoundError:
+                pass
 
 
 class XgmiAllReduce:
@@ -108,7 +172,11 @@ class XgmiAllReduce:
         # 6) streams: one per peer (parallel links) + the reduction stream
         self.comm = torch.cuda.Stream(device=self.dev)
         self.copy = {r: torch.cuda.Stream(device=self.dev) for r in range(W) if r != self.rank}
-        # 7) comm thread
+        # 7) host sequence words: [ready b | reduced b | step]
+        self.nb = nb
+        self.seq = 1  # current step's sequence number (published values start at 1)
+        self.hseq = _HostSeq(self.rank, W, 2 * nb + 1, self.hgroup)
+        # 8) comm thread
         self.q: "queue.Queue" = queue.Queue()
         self.error = None
         self.works: List[_Work] = []
@@ -144,7 +212,11 @@ class XgmiAllReduce:
             try:
                 if b == "step":
                     self.C.event_record(self.ev_step, self.comm.cuda_stream)
-                    dist.barrier(group=self.hgroup)
+                    self.hseq.publish(2 * self.nb, self.seq)
+                    for r in range(self.world):
+                        if r != self.rank:
+                            self.hseq.wait(r, 2 * self.nb, self.seq)
+                    self.seq += 1
                 else:
                     self._bucket(b)
             except Exception as e:  # surfaced by the waiter
@@ -160,10 +232,12 @@ class XgmiAllReduce:
         sl = self.slices[b]
         s0, s1 = sl[me]
         n = s1 - s0
-        dist.barrier(group=self.hgroup)  # every rank recorded ev_ready[b]
+        hs, seq = self.hseq, self.seq
+        hs.publish(b, seq)  # ev_ready[b] was recorded (launch) before this bucket was queued
         # reduce-scatter: pull my slice from every peer, all links at once
         for r, cs in self.copy.items():
             h = cs.cuda_stream
+            hs.wait(r, b, seq)  # peer r recorded its ev_ready[b] of this step
             C.stream_wait_event(h, self.peer_ready[r][b])
             cs.wait_event(self.ev_sum)  # staging reused: previous bucket's reduction consumed it
             C.copy_async(self._stage(r), self.peer_base[r] + s0 * es, n * es, h)
@@ -175,10 +249,11 @@ class XgmiAllReduce:
         C.sum_slices(srcs, self.peer_base[me] + s0 * es, n, self.dtype, comm.cuda_stream)
         self.ev_sum.record(comm)
         C.event_record(self.ev_rs[b], comm.cuda_stream)
-        dist.barrier(group=self.hgroup)  # every rank recorded ev_rs[b]
+        hs.publish(self.nb + b, seq)
         # all-gather: pull each owner's reduced slice into my buffer
         for r, cs in self.copy.items():
             h = cs.cuda_stream
+            hs.wait(r, self.nb + b, seq)  # peer r recorded its ev_rs[b] of this step
             C.stream_wait_event(h, self.peer_rs[r][b])
             p0, p1 = sl[r]
             C.copy_async(self.peer_base[me] + p0 * es, self.peer_base[r] + p0 * es, (p1 - p0) * es, h)

@@ -174,3 +174,34 @@ def test_bench_launch_command():
     assert bench.launch_command(["--gpus", "8"], 8, {"WORLD_SIZE": "8"}) == []
     assert bench.launch_command([], 1, {}) == []
     assert bench.launch_command(["--gpus", "4"], 4, {"SLURM_PROCID": "0", "SLURM_NTASKS": "4"}) == []
+
+
+def _hostseq_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from pyrecover_amd.parallel.xgmi import _HostSeq
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    hs = _HostSeq(rank, world, 3, None)
+    name = hs.shm.name
+    for seq in range(1, 51):  # ping-pong: each slot published then awaited by every peer
+        for slot in range(3):
+            hs.publish(slot, seq)
+            for r in range(world):
+                hs.wait(r, slot, seq, timeout=30)
+    dist.barrier()
+    hs.close()
+    dist.barrier()
+    with open(os.path.join(out_dir, f"hs_{rank}.txt"), "w") as f:
+        f.write(f"{name} {os.path.exists('/dev/shm/' + name)}")
+    dist.destroy_process_group()
+
+
+def test_xgmi_host_sequence_words(tmp_path):
+    """The shared-memory sequence words that order the xGMI backend's IPC events (no gloo barrier
+    per bucket): 2 processes, 150 publish/wait rounds, segment unlinked after close."""
+    mp.spawn(_hostseq_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        name, exists = open(tmp_path / f"hs_{r}.txt").read().split()
+        assert name.startswith("pra_xgmi_") and exists == "False"
