@@ -231,7 +231,7 @@ struct Piece {
 // besides the reference's whole-file `.md5` every checkpoint file carries the MD5 of each
 // 256 MiB segment, written and verified by many threads in parallel.
 constexpr uint64_t kSegBytes = 256ull << 20;
-constexpr int kWriters = 8;
+constexpr int kWriters = 16;  // 16 vs 8: vanilla save 9.4 -> 8.0 s, sharded 5.6 -> 5.2 s at 7B (profiles/ckpt_threads_ab_r2)
 
 inline std::string digest_hex(EVP_MD_CTX* ctx) {
   unsigned char dig[EVP_MAX_MD_SIZE];
