@@ -157,13 +157,15 @@ class Transformer(nn.Module):
         return fc
 
     def _apply(self, fn, recurse=True):
-        out = super()._apply(fn, recurse)
-        # dtype casts must not touch the rotation tables: rebuild them (complex64 / fp32) on the
-        # buffers' (possibly new) device from the config, exactly as at construction.
-        dev = self.rope_tab.device
-        if self.freqs_cis.dtype != torch.complex64 or self.rope_tab.dtype != torch.float32:
-            self.freqs_cis = self._precompute_freqs_cis().to(dev)
-            self.rope_tab = rope_table(self.freqs_cis)
+        # the rotation tables never take the model's dtype: keep them out of `fn` (a complex
+        # buffer cast to a real dtype would lose its imaginary part) and only follow the device
+        tables = {k: self._buffers.pop(k) for k in ("freqs_cis", "rope_tab")}
+        try:
+            out = super()._apply(fn, recurse)
+        finally:
+            dev = self.tok_embeddings.weight.device
+            for k, t in tables.items():
+                self._buffers[k] = t.to(dev)
         if self.flat is not None and any(p.data.data_ptr() < self.flat.data.data_ptr() or
                                          p.data.data_ptr() >= self.flat.data.data_ptr() + self.flat.state_bytes()
                                          for p in self.parameters()):

@@ -85,6 +85,17 @@ TN_WGRAD = os.environ.get("PYRECOVER_TN_WGRAD", "1") == "1"
 TN_WGRAD_WO = TN_WGRAD and os.environ.get("PYRECOVER_TN_WGRAD_WO", "1") == "1"
 
 
+# Shape limits of the HIP kernels (outside them the op runs the torch math of ops/reference.py on
+# the same device, like fp64): norms hold a row in registers (D <= 8192, 16-B chunks), embedding
+# rows and SwiGLU halves move as 16-B vectors.
+def _norm_hip(x):
+    return _ext.hip(x) and x.shape[-1] % 8 == 0 and x.shape[-1] <= 8192
+
+
+def _vec_hip(t, width):
+    return _ext.hip(t) and width % 8 == 0
+
+
 def _tn_ok(t):
     return (_ext.hip16(t) and t.dim() == 2 and t.element_size() == 2 and t.stride(1) == 1 and t.size(0) % 64 == 0
             and t.size(1) % 64 == 0 and t.stride(0) % 8 == 0)
@@ -106,7 +117,7 @@ class _Embedding(torch.autograd.Function):
         ctx.slot = slot
         ctx.save_for_backward(ids)
         ctx.shape = weight.shape
-        if _ext.hip(weight):
+        if _vec_hip(weight, weight.shape[1]):
             return _ext.require_for(weight).embedding_fwd(ids.contiguous(), weight)
         return torch.nn.functional.embedding(ids, weight)
 
@@ -116,7 +127,7 @@ class _Embedding(torch.autograd.Function):
         slot = ctx.slot
         buf, acc = slot.begin(dout)
         V, D = ctx.shape
-        if _ext.hip(dout):
+        if _vec_hip(dout, D):
             _ext.require_for(dout).embedding_bwd(ids.contiguous(), dout.contiguous(), buf.view(V, D), acc)
         else:
             g = buf.view(V, D)
@@ -139,7 +150,7 @@ class _AddRMSNorm(torch.autograd.Function):
     def forward(ctx, x, delta, weight, slot, eps):
         ctx.slot = slot
         ctx.has_delta = delta is not None
-        if _ext.hip(x):
+        if _norm_hip(x):
             h, y, rstd = _ext.require_for(x).rmsnorm_fwd(x.contiguous(), delta.contiguous() if delta is not None else None,
                                                          weight, eps)
         else:
@@ -158,7 +169,7 @@ class _AddRMSNorm(torch.autograd.Function):
             dh, dy = None, grads[0]
         slot = ctx.slot
         buf, acc = slot.begin(dy)
-        if _ext.hip(dy):
+        if _norm_hip(dy):
             dx = _ext.require_for(dy).rmsnorm_bwd(dy.contiguous(), h, weight, rstd,
                                                   dh.contiguous() if dh is not None else None, buf, acc)
         else:
@@ -188,7 +199,7 @@ class _AddLayerNorm(torch.autograd.Function):
         ctx.slot = slot
         ctx.has_delta = delta is not None
         ctx.eps = eps
-        if _ext.hip(x):
+        if _norm_hip(x):
             h, y, mean, rstd = _ext.require_for(x).layernorm_fwd(
                 x.contiguous(), delta.contiguous() if delta is not None else None, weight, bias, eps)
         else:
@@ -207,7 +218,7 @@ class _AddLayerNorm(torch.autograd.Function):
         slot = ctx.slot
         buf, acc = slot.begin(dy)
         D = h.shape[-1]
-        if _ext.hip(dy):
+        if _norm_hip(dy):
             dx = _ext.require_for(dy).layernorm_bwd(dy.contiguous(), h, weight, mean, rstd,
                                                     dh.contiguous() if dh is not None else None, buf, acc)
         else:
@@ -234,11 +245,17 @@ def add_layer_norm(x, delta, weight, bias, slot, eps):
 
 
 # ---------------------------------------------------------------------------------------
+def _attn_hip(q, k):
+    """The MFMA kernels: bf16/fp16, head_dim 64 or 128, whole GQA groups, 16-B aligned rows."""
+    return (_ext.hip16(q) and q.shape[-1] in (64, 128) and q.shape[2] % k.shape[2] == 0
+            and all(t.stride(-1) == 1 and t.stride(1) % 8 == 0 for t in (q, k)))
+
+
 def _attn_fwd(q, k, v, scale, causal):
-    """HIP flash attention for bf16/fp16 GPU tensors (any S: the binding zero-pads sequences
-    that do not tile); otherwise torch SDPA in fp32 (fp64 for fp64 inputs), as the reference's
-    non-flash path (reference model.py:192, 227). Returns (o, lse or None)."""
-    if _ext.hip16(q):
+    """HIP flash attention for bf16/fp16 GPU tensors with head_dim 64/128 (any S: the binding
+    zero-pads sequences that do not tile); otherwise torch SDPA in fp32 (fp64 for fp64 inputs),
+    as the reference's non-flash path (reference model.py:192, 227). Returns (o, lse or None)."""
+    if _attn_hip(q, k):
         return _ext.require_for(q).attn_fwd(q, k, v, scale, causal)
     ct = torch.promote_types(q.dtype, torch.float32)
     with torch.no_grad():
@@ -247,7 +264,7 @@ def _attn_fwd(q, k, v, scale, causal):
 
 
 def _attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, causal):
-    if _ext.hip16(q):
+    if lse is not None and _attn_hip(q, k):
         _ext.require_for(q).attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, causal)
         return
     ct = torch.promote_types(q.dtype, torch.float32)
@@ -272,7 +289,7 @@ class _AttentionBlock(torch.autograd.Function):
         x2 = x.reshape(T, dim)
         qkv = torch.mm(x2, w_qkv.t())
         nq, nk = Hq * D, Hkv * D
-        if _ext.hip(qkv):
+        if _ext.hip(qkv) and D % 8 == 0:
             _ext.require_for(qkv).rope_(qkv, nq + nk, tab, D, S, 0, False)
         else:
             ref.rope_inplace_2d(qkv, nq + nk, tab, D, S)
@@ -314,14 +331,14 @@ class _AttentionBlock(torch.autograd.Function):
         dk = dqkv[:, nq:nq + nk].view(B, S, Hkv, D)
         dv = dqkv[:, nq + nk:].view(B, S, Hkv, D)
         _attn_bwd(q, k, v, o, do, lse, dq, dk, dv, ctx.scale, causal)
-        if TN_WGRAD and _tn_ok(dqkv) and _tn_ok(x2) and T % S == 0:
+        if TN_WGRAD and _tn_ok(dqkv) and _tn_ok(x2) and T % S == 0 and D % 8 == 0:
             # inverse RoPE in place + dqkv^T in one pass, for the K-contiguous weight-grad GEMM
             C = _ext.require_for(dqkv)
             dqkvT = C.rope_t_(dqkv, nq + nk, tab, D, S, True)
             dx = torch.mm(dqkv, w_qkv_t.t()) if w_qkv_t is not None else torch.mm(dqkv, w_qkv)
             slot_qkv.mm_(dqkvT, C.transpose2d(x2).t(), tuple(w_qkv.shape))
         else:
-            if _ext.hip(dqkv):
+            if _ext.hip(dqkv) and D % 8 == 0:
                 _ext.require_for(dqkv).rope_(dqkv, nq + nk, tab, D, S, 0, True)
             else:
                 ref.rope_inplace_2d(dqkv, nq + nk, tab, D, S, inverse=True)
@@ -339,7 +356,7 @@ def attention_block(x, w_qkv, w_o, slot_qkv, slot_o, tab, dims, params, w_t=None
 
 # ---------------------------------------------------------------------------------------
 def _swiglu_fwd(gu):
-    if _ext.hip(gu):
+    if _vec_hip(gu, gu.shape[1] // 2) and gu.shape[1] % 16 == 0:
         return _ext.require_for(gu).swiglu_fwd(gu)
     F = gu.shape[1] // 2
     g, u = ref.up(gu[:, :F]), ref.up(gu[:, F:])
@@ -347,7 +364,7 @@ def _swiglu_fwd(gu):
 
 
 def _swiglu_bwd_(da, gu):
-    if _ext.hip(gu):
+    if _vec_hip(gu, gu.shape[1] // 2) and gu.shape[1] % 16 == 0:
         return _ext.require_for(gu).swiglu_bwd(da, gu, gu)
     F = gu.shape[1] // 2
     dg, du = ref.swiglu_bwd_ref(da, gu[:, :F], gu[:, F:])

@@ -231,3 +231,31 @@ def test_train_py_model_dtypes(cuda, tmp_path, dtype):
     r2 = subprocess.run(args2 + ["--resume-from-checkpoint", "latest"], capture_output=True, text=True, timeout=300,
                         cwd=root)
     assert r2.returncode == 0, (r2.stdout + r2.stderr)[-4000:]
+
+
+@pytest.mark.parametrize("over", [{"dim": 96, "n_heads": 3, "n_kv_heads": 1},  # head_dim 32 (SDPA path)
+                                  {"dim": 200, "n_heads": 2, "n_kv_heads": 2, "multiple_of": 20},  # D % 8 != 0
+                                  {"dim": 9216, "n_heads": 72, "n_kv_heads": 8, "n_layers": 1,
+                                   "vocab_size": 128}])  # RMSNorm row > 8192
+def test_shapes_outside_the_hip_kernels_fall_back(cuda, over):
+    """Shapes the HIP kernels do not take (head_dim not 64/128, rows not 16-B multiples, norm rows
+    > 8192) run torch math on the GPU for those ops and still match the fp32 reference."""
+    torch.manual_seed(0)
+    a = get_preset("llama-micro", seq_len=64, **over)
+    cpu = Transformer(a)
+    B, S = 2, 64
+    tok = torch.randint(0, a.vocab_size, (B, S))
+    lab = torch.randint(0, a.vocab_size, (B, S))
+    loss_ref = R.cross_entropy_ref(ref_forward(cpu, tok), lab)
+    loss_ref.backward()
+    gpu = Transformer(a)
+    gpu.load_state_dict(cpu.state_dict())
+    gpu = gpu.to(cuda, torch.bfloat16)
+    gpu.flatten_().zero_grad()
+    loss = gpu(tok.to(cuda), labels=lab.to(cuda))
+    loss.backward()
+    assert abs(loss.item() - loss_ref.item()) < 2e-2 * loss_ref.item()
+    for n, p in gpu.named_parameters():
+        r = dict(cpu.named_parameters())[n].grad
+        rel = ((p.grad.float().cpu() - r).norm() / r.norm().clamp_min(1e-12)).item()
+        assert rel < 6e-2, (n, rel)
