@@ -27,7 +27,11 @@ def main():
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--fwd", action="store_true", help="time the forward instead")
+    ap.add_argument("--set", default="", help="fixed VAR=VAL[,VAR=VAL] for every arm")
     a = ap.parse_args()
+    for kv in filter(None, a.set.split(",")):
+        k_, v_ = kv.split("=", 1)
+        os.environ[k_] = v_
     from pyrecover_amd import _ext
 
     C = _ext.native()
