@@ -396,8 +396,10 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const T* __restrict__
                                                            long ldk, long ldv, long ldo, float scale_log2, float thr) {
   constexpr int KT = 64, QT = 32 * NW;
   constexpr int NKS = D / 16, NDB = D / 32, TILE = KT * D;
-  // (K V) x 3, one __shared__ object per ring slot (fwd_w_kernel: per-object alias scopes keep the
-  // reads of slot t from waiting for the LDS-DMA into slot t + 2)
+  // (K V) x 3, one __shared__ object per ring slot: the LDS lowering gives each object its own alias
+  // scope, so the reads of slot t (ds_read_b64_tr_b16 in particular) are not made to wait
+  // (vmcnt(0)) for the LDS-DMA still filling slot t + 2 -- with one array the compiler drained the
+  // in-flight DMA before the first transposed read of every tile (9 mid-loop vmcnt(0); now 0)
   __shared__ __attribute__((aligned(16))) T kv0[2 * TILE];
   __shared__ __attribute__((aligned(16))) T kv1[2 * TILE];
   __shared__ __attribute__((aligned(16))) T kv2[2 * TILE];
@@ -577,264 +579,6 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const T* __restrict__
     const float inv = 1.f / l_i;
     store_rows16<T, NDB>(o, inv, O + ((long)b * S + qrow) * ldo + hq * D, qrow < S, h2);
     if (qrow < S && h2 == 0) LSE[((long)b * Hq + hq) * S + qrow] = (m_i + __log2f(l_i)) * 0.69314718055994531f;
-  }
-}
-
-// ======================================================================================
-// Forward, one wave per SIMD, 64 query rows per wave (fwd_w_kernel): block = 4 waves x 64 queries
-// (256 rows, as fwd_p_kernel), __launch_bounds__(256, 1) so each wave owns the whole register
-// file. Every K fragment read from LDS feeds two MFMAs (query blocks a and b), and so does every
-// V^T fragment; the wave's own instruction stream carries both the MFMAs and the softmax VALU (no
-// partner wave to alternate with: cdna guide 'one wave per SIMD', MI355X_MICROARCH 'single-issue
-// instructions hidden per MFMA gap').
-// Register budget: MFMA C/D and VALU operands must sit in the 256 architectural VGPRs (spilling the
-// O accumulators to AGPRs costs two copies per element per tile), so the wave's Q lives in LDS
-// (64 KB for the block, next to the 96 KB K/V ring: the CU's whole 160 KB) and the software
-// pipeline runs over 32-key sub-tiles (two per 64-key LDS tile):
-//   O (128) + S of sub-tile s (32) + S of s+1 (32) + packed P (16) + fragments ~ 250 VGPRs.
-// Sub-tile s (exact deferred rescale, as fwd_p_kernel):
-//   phase A (NKS regions):  S(s+1) = K Q^T, blocks a and b         | exp of P_a(s), first half of P_b(s)
-//   phase B (2 NDB regions): O^T += V^T P(s), blocks a and b        | second half of P_b(s) (while the
-//                           first key k-step runs), row max of S(s+1)
-// The split of the exponentials balances issue between the phases: phase A regions carry 3
-// softmax elements beside their 2 MFMAs and 3 fragment reads, phase B regions 2 plus the max.
-// ======================================================================================
-template <typename T, int D, bool CAUSAL>
-__global__ __launch_bounds__(256, 1) void fwd_w_kernel(const T* __restrict__ Q, const T* __restrict__ K,
-                                                       const T* __restrict__ V, T* __restrict__ O,
-                                                       float* __restrict__ LSE, int S, int Hq, int Hkv, long ldq,
-                                                       long ldk, long ldv, long ldo, float scale_log2, float thr) {
-  constexpr int NW = 4, KT = 64, QW = 64, QT = NW * QW;
-  constexpr int NKS = D / 16, NDB = D / 32, TILE = KT * D;
-  constexpr int RA = NKS, RB = 2 * NDB;
-  constexpr int NEA = 24, EA = NEA / RA;  // exponentials in phase A: all 16 of P_a, 8 of P_b
-  static_assert(EA * RA == NEA, "phase A split");
-  // (K V) x 3 | Q of the block (256 rows). One __shared__ object per ring slot: the LDS lowering
-  // gives each its own alias scope, so a read of slot t is not made to wait (vmcnt(0)) for the
-  // LDS-DMA still filling slot t + 2 -- with one array every ds_read_b64_tr_b16 after the DMA
-  // issue drained it mid-tile.
-  __shared__ __attribute__((aligned(16))) T kv0[2 * TILE];
-  __shared__ __attribute__((aligned(16))) T kv1[2 * TILE];
-  __shared__ __attribute__((aligned(16))) T kv2[2 * TILE];
-  __shared__ __attribute__((aligned(16))) T Qs[QT * D];
-
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h2 = lane >> 5, l32 = lane & 31;
-  const int nqt = (S + QT - 1) / QT;
-  const int BH = gridDim.x / nqt;
-  const int qt = nqt - 1 - (int)(blockIdx.x / BH);  // heavy (late) query tiles first
-  const int bh = blockIdx.x % BH;
-  const int hq = bh % Hq, b = bh / Hq;
-  const int hk = hq / (Hq / Hkv);
-  const int q0 = qt * QT, qw = q0 + wid * QW;
-
-  const T* Qb = Q + (long)b * S * ldq + hq * D;
-  const T* Kb = K + (long)b * S * ldk + hk * D;
-  const T* Vb = V + (long)b * S * ldv + hk * D;
-
-  LaneOff<T, D> lo;
-  lo.init(lane);
-  const int qra = qw + l32, qrb = qra + 32;  // this lane's query of block a / b
-
-  f32x16 oa[NDB], ob[NDB];
-#pragma unroll
-  for (int i = 0; i < NDB; ++i) { oa[i] = f32x16{}; ob[i] = f32x16{}; }
-  float ma = -INFINITY, mb = -INFINITY, la = 0.f, lb = 0.f;
-
-  const int kend = CAUSAL ? min(S, q0 + QT) : S;
-  const int nkt = (kend + KT - 1) / KT;
-  const int lastw = CAUSAL ? min(nkt - 1, (qw + QW - 1) / KT) : nkt - 1;  // this wave's last tile
-  const int lasts = 2 * lastw + 1;                                         // ... and 32-key sub-tile
-
-  GStage<T, D, KT, NW> gk, gv;  // LDS-DMA (S % 64 == 0: tiles are always full)
-  gk.init(ldk);
-  gv.init(ldv);
-  auto slot = [&](int t) { return t == 0 ? kv0 : kv1; };  // prologue tiles 0 and 1 only
-  {  // the block's 256 query rows, by LDS-DMA (rows past S re-read the last row; never stored)
-    GStage<T, D, QT, NW> gq;
-    gq.init(ldq);
-#pragma unroll
-    for (int i = 0; i < GStage<T, D, QT, NW>::NI; ++i) {
-      const int row = gq.off[i] / (int)ldq;
-      if (q0 + row >= S) gq.off[i] += (S - 1 - q0 - row) * (int)ldq;
-    }
-    gq.issue(Qb + (long)q0 * ldq, Qs);
-  }
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-    if (t < nkt) {
-      gk.issue(Kb + (long)t * KT * ldk, slot(t));
-      gv.issue(Vb + (long)t * KT * ldv, slot(t) + TILE);
-    }
-  __syncthreads();
-  const T* const Qw = Qs + wid * QW * D;  // this wave's 64 rows: block a = rows 0..31, b = 32..63
-
-  // masks keys beyond the query: key kb + crow(r, h2) vs query qr
-  auto mask = [&](f32x16& sv, int kb, int qr) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r)
-      if (kb + crow(r, h2) > qr) sv[r] = -INFINITY;
-  };
-  auto rowmax = [&](const f32x16& sv) {
-    float mx = -INFINITY;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sv[r]);
-    return half_max(mx) * scale_log2;
-  };
-
-  // scores of the sub-tile being finished (query block a / b, 32 keys)
-  f32x16 ca = f32x16{}, cb = f32x16{};
-  if (lastw >= 0) {
-    const T* Kt = slot(0);
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-      const V8<T> kf = lo.rowk(Kt, 0, ks);
-      ca = mfma(kf, lo.rowk(Qw, 0, ks), ca);
-      cb = mfma(kf, lo.rowk(Qw, 32, ks), cb);
-    }
-    if (CAUSAL && lasts <= 1) {  // (lastw == 0: sub-tile 0 is on the diagonal)
-      mask(ca, 0, qra);
-      mask(cb, 0, qrb);
-    }
-    ma = rowmax(ca);
-    mb = rowmax(cb);
-  }
-
-  // one 32-key sub-tile: HS = which half of the LDS tile (compile-time, so every LDS operand
-  // address is a lane-constant base plus an immediate)
-  auto sub = [&](const T* Kn, auto kn_off_c, const T* Vt, auto hs_c, int s) __attribute__((always_inline)) {
-    constexpr int KNO = decltype(kn_off_c)::value, HS = decltype(hs_c)::value;
-    auto iter = [&](auto next_c, auto diag_c) __attribute__((always_inline)) {
-      constexpr bool NEXT = decltype(next_c)::value, DIAG = decltype(diag_c)::value;
-      f32x16 na = f32x16{}, nb = f32x16{};
-      float rsa = 0.f, rsb = 0.f, mxa = -INFINITY, mxb = -INFINITY;
-      auto expo = [&](int e) {  // element e of [P_a(0..15), P_b(0..15)]
-        if (e < 16) {
-          ca[e] = fexp2(fmaf(ca[e], scale_log2, -ma));
-          rsa += ca[e];
-        } else {
-          cb[e - 16] = fexp2(fmaf(cb[e - 16], scale_log2, -mb));
-          rsb += cb[e - 16];
-        }
-      };
-      // phase A: region ks: na += K[ks] Qa[ks], nb += K[ks] Qb[ks]; fragments one region ahead
-      V8<T> kc = lo.rowk(Kn, KNO, 0), qac = lo.rowk(Qw, 0, 0), qbc = lo.rowk(Qw, 32, 0);
-#pragma unroll
-      for (int j = 0; j < RA; ++j) {
-        V8<T> kn = kc, qan = qac, qbn = qbc;
-        if (NEXT && j + 1 < RA) {
-          kn = lo.rowk(Kn, KNO, j + 1);
-          qan = lo.rowk(Qw, 0, j + 1);
-          qbn = lo.rowk(Qw, 32, j + 1);
-        }
-        if (NEXT) {
-          na = mfma(kc, qac, na);
-          nb = mfma(kc, qbc, nb);
-        }
-#pragma unroll
-        for (int e = 0; e < EA; ++e) expo(j * EA + e);
-        kc = kn;
-        qac = qan;
-        qbc = qbn;
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      la += half_sum(rsa);
-      const V8<T> pa0 = pack8<T>(ca, 0), pa1 = pack8<T>(ca, 1), pb0 = pack8<T>(cb, 0);
-      if (NEXT && DIAG) {
-        mask(na, (s + 1) * 32, qra);
-        mask(nb, (s + 1) * 32, qrb);
-      }
-      // phase B: region j = (key k-step k2 = j / NDB, d block db = j % NDB); one V^T fragment
-      // for both query blocks, read two regions ahead
-      constexpr int VR = 32 * HS;  // the sub-tile's first key row in the V tile
-      V8<T> vc = lo.tr(Vt, VR, 0), vn = lo.tr(Vt, VR + (1 / NDB) * 16, 1 % NDB);
-      V8<T> pb1;
-#pragma unroll
-      for (int j = 0; j < RB; ++j) {
-        V8<T> vnn = vn;
-        if (j + 2 < RB) vnn = lo.tr(Vt, VR + ((j + 2) / NDB) * 16, (j + 2) % NDB);
-        const int k2 = j / NDB, db = j % NDB;
-        oa[db] = mfma(vc, k2 ? pa1 : pa0, oa[db]);
-        if (k2 == 0) {
-          ob[db] = mfma(vc, pb0, ob[db]);
-          // the second half of P_b (keys 16..31 of the sub-tile), used from k2 = 1 on
-#pragma unroll
-          for (int e = 0; e < (16 - (NEA - 16)) / NDB; ++e) expo(NEA + db * ((16 - (NEA - 16)) / NDB) + e);
-          if (db == NDB - 1) {
-            pb1 = pack8<T>(cb, 1);
-            lb += half_sum(rsb);
-          }
-        } else {
-          ob[db] = mfma(vc, pb1, ob[db]);
-        }
-        if (NEXT) {
-#pragma unroll
-          for (int e = 0; e < 32 / RB; ++e) {
-            const int i = j * (32 / RB) + e;
-            if (i < 16) mxa = fmaxf(mxa, na[i]);
-            else mxb = fmaxf(mxb, nb[i - 16]);
-          }
-        }
-        vc = vn;
-        vn = vnn;
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (NEXT) {
-        mxa = half_max(mxa) * scale_log2;
-        mxb = half_max(mxb) * scale_log2;
-        if (!__all(mxa <= ma + thr)) {  // deferred rescale (sub-tile s's P.V is already in O)
-          const float m_new = fmaxf(ma, mxa);
-          const float alpha = fexp2(ma - m_new);
-          la *= alpha;
-#pragma unroll
-          for (int i = 0; i < NDB; ++i) oa[i] *= alpha;
-          ma = m_new;
-        }
-        if (!__all(mxb <= mb + thr)) {
-          const float m_new = fmaxf(mb, mxb);
-          const float alpha = fexp2(mb - m_new);
-          lb *= alpha;
-#pragma unroll
-          for (int i = 0; i < NDB; ++i) ob[i] *= alpha;
-          mb = m_new;
-        }
-        ca = na;
-        cb = nb;
-      }
-    };
-    // causal: the wave's last two sub-tiles (its 64-key diagonal tile) need the mask
-    if (s + 1 > lasts) iter(std::false_type{}, std::false_type{});
-    else if (CAUSAL && s + 1 >= lasts - 1) iter(std::true_type{}, std::true_type{});
-    else iter(std::true_type{}, std::false_type{});
-  };
-
-  auto body = [&](auto cur_c, int t) __attribute__((always_inline)) {
-    constexpr int CUR = decltype(cur_c)::value;
-    T* const s_cur = CUR == 0 ? kv0 : CUR == 1 ? kv1 : kv2;
-    T* const s_nxt = CUR == 0 ? kv1 : CUR == 1 ? kv2 : kv0;
-    T* const s_nn = CUR == 0 ? kv2 : CUR == 1 ? kv0 : kv1;
-    if (t + 2 < nkt) {  // LDS-DMA of tile t + 2 into the slot tile t - 1 vacated
-      gk.issue(Kb + (long)(t + 2) * KT * ldk, s_nn);
-      gv.issue(Vb + (long)(t + 2) * KT * ldv, s_nn + TILE);
-    }
-    if (t <= lastw) {
-      // sub-tile 2t: S of 2t+1 comes from the upper half of this tile; sub-tile 2t+1: S of 2t+2
-      // from the lower half of the next tile (landed at the previous barrier)
-      sub(s_cur, IC<32>{}, s_cur + TILE, IC<0>{}, 2 * t);
-      sub(s_nxt, IC<0>{}, s_cur + TILE, IC<1>{}, 2 * t + 1);
-    }
-    __syncthreads();  // tile t + 2 landed (vmcnt(0) before the barrier); tile t's slot is free
-  };
-  for (int t = 0; t < nkt; t += 3) {
-    body(IC<0>{}, t);
-    if (t + 1 < nkt) body(IC<1>{}, t + 1);
-    if (t + 2 < nkt) body(IC<2>{}, t + 2);
-  }
-
-  store_rows16<T, NDB>(oa, 1.f / la, O + ((long)b * S + qra) * ldo + hq * D, qra < S, h2);
-  store_rows16<T, NDB>(ob, 1.f / lb, O + ((long)b * S + qrb) * ldo + hq * D, qrb < S, h2);
-  if (h2 == 0) {
-    if (qra < S) LSE[((long)b * Hq + hq) * S + qra] = (ma + __log2f(la)) * 0.69314718055994531f;
-    if (qrb < S) LSE[((long)b * Hq + hq) * S + qrb] = (mb + __log2f(lb)) * 0.69314718055994531f;
   }
 }
 
@@ -1241,7 +985,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
   constexpr int KT = 64, QT = 32 * NW;
   constexpr int NKS = D / 16, NDB = D / 32, TILE = KT * D;
   // K0 V0 | K1 V1: one __shared__ object per buffer, so the reads of one buffer do not wait
-  // (vmcnt(0)) for the LDS-DMA filling the other (per-object alias scopes; see fwd_w_kernel)
+  // (vmcnt(0)) for the LDS-DMA filling the other (per-object alias scopes; see fwd_p_kernel)
   __shared__ __attribute__((aligned(16))) T kvb0[2 * TILE];
   __shared__ __attribute__((aligned(16))) T kvb1[2 * TILE];
 
@@ -1466,15 +1210,8 @@ hipError_t attn_fwd_t(const void* q, const void* k, const void* v, void* o, floa
   // 0 = exact rescale at every growth.
   const char* ft = getenv("PRA_FWD_THR");
   const float thr = ft ? (float)atof(ft) : 8.f;
-  // PRA_FWD_W=1 (read per call): the one-wave-per-SIMD 64-row kernel (no key bound either)
-  const char* fw = getenv("PRA_FWD_W");
-  // (causal only: the full-attention instantiation spills at D = 128)
-  const bool wide = causal && (fw ? atoi(fw) != 0 : false);
 #define LAUNCH(DD, CC)                                                                                        \
-  if (wide)                                                                                                   \
-    hipLaunchKernelGGL((fwd_w_kernel<T, DD, true>), dim3(nqt * Hq * B), dim3(256), 0, st, (const T*)q,       \
-                       (const T*)k, (const T*)v, (T*)o, lse, S, Hq, Hkv, ldq, ldk, ldv, ldo, sl2, thr);            \
-  else if (pipe)                                                                                              \
+  if (pipe)                                                                                                   \
     hipLaunchKernelGGL((fwd_p_kernel<T, DD, CC, NW>), grid, block, 0, st, (const T*)q, (const T*)k,         \
                        (const T*)v, (T*)o, lse, S, Hq, Hkv, ldq, ldk, ldv, ldo, sl2, thr);                  \
   else                                                                                                        \

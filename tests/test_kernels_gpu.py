@@ -188,11 +188,10 @@ def _qkv(cuda, B, S, Hq, Hkv, D, seed=0, scale=1.0):
 @pytest.mark.parametrize("B,S,Hq,Hkv,D", [(1, 256, 4, 4, 128), (2, 512, 8, 2, 128), (1, 384, 4, 1, 64),
                                           (1, 128, 2, 2, 64), (1, 192, 4, 2, 128)])
 @pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("pipe", ["0", "1", "w"])
+@pytest.mark.parametrize("pipe", ["0", "1"])
 def test_attention_fwd(cuda, monkeypatch, pipe, B, S, Hq, Hkv, D, causal):
-    """Every forward kernel (PRA_FWD_PIPE: fwd_kernel / cross-tile pipelined fwd_p_kernel;
-    PRA_FWD_W: the one-wave-per-SIMD 64-row fwd_w_kernel, causal only)."""
-    _fwd_variant(monkeypatch, pipe)
+    """Both forward kernels (PRA_FWD_PIPE: fwd_kernel / cross-tile pipelined fwd_p_kernel)."""
+    monkeypatch.setenv("PRA_FWD_PIPE", pipe)
     C = _ext.native()
     _, q, k, v = _qkv(cuda, B, S, Hq, Hkv, D)
     scale = 1 / math.sqrt(D)
@@ -202,15 +201,13 @@ def test_attention_fwd(cuda, monkeypatch, pipe, B, S, Hq, Hkv, D, causal):
     assert (lse - lse_ref).abs().max().item() < 1e-3
 
 
-def _fwd_variant(monkeypatch, pipe):
-    monkeypatch.setenv("PRA_FWD_PIPE", "1" if pipe == "w" else pipe)
-    monkeypatch.setenv("PRA_FWD_W", "1" if pipe == "w" else "0")
-
-
-@pytest.mark.parametrize("pipe", ["0", "1", "w"])
-def test_attention_fwd_rescale_spike(cuda, monkeypatch, pipe):
-    """Forces the online-softmax running max to jump at a late key tile (rule 26)."""
-    _fwd_variant(monkeypatch, pipe)
+@pytest.mark.parametrize("pipe", ["0", "1"])
+@pytest.mark.parametrize("thr", ["0", "8"])
+def test_attention_fwd_rescale_spike(cuda, monkeypatch, pipe, thr):
+    """Forces the online-softmax running max to jump at a late key tile (rule 26), with the exact
+    rescale (PRA_FWD_THR=0) and the default deferred threshold."""
+    monkeypatch.setenv("PRA_FWD_PIPE", pipe)
+    monkeypatch.setenv("PRA_FWD_THR", thr)
     C = _ext.native()
     B, S, H, D = 1, 512, 2, 128
     _, q, k, v = _qkv(cuda, B, S, H, H, D, seed=3)
