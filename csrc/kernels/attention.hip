@@ -1290,8 +1290,12 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
     const int impl_env = impl_s ? atoi(impl_s) : -1;
     const int nw = (nw_env == 4 || S % 256) ? 4 : 8;
     // D = 64: 64 KB of LDS and <= 256 VGPRs, so two blocks share a CU and hide each other's prologue
-    // (B16 S2048 H16: 0.74 -> 0.68 ms bwd)
-    const bool p2 = impl_env == 1 || (impl_env < 0 && (D == 64 || (long)(Hq / Hkv) * S >= 8192));
+    // (B16 S2048 H16: 0.74 -> 0.68 ms bwd). At D = 128 the pipelined kernel wins only while the
+    // two-wave kernel's grid ((S/256) Hkv B blocks, one per CU) is at most one round of the chip's
+    // 256 CUs, where its causal work imbalance is exposed: S 8192 GQA 32/8 bwd B1 2.56 -> 1.98 ms
+    // with p2, but B4 7.30 (two-wave) vs 7.89 ms (p2) (profiles/attn_dkdv_select_r2.log).
+    const long grid2 = (long)(S / 256) * Hkv * B;
+    const bool p2 = impl_env == 1 || (impl_env < 0 && (D == 64 || ((long)(Hq / Hkv) * S >= 8192 && grid2 <= 256)));
     if (p2 && nw_env == 0) {
       dim3 g1((S / 128) * Hkv * B);
 #define LAUNCH1(DD, CC)                                                                                       \
