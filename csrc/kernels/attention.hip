@@ -175,26 +175,30 @@ struct Stage {
 // writes 1 KiB per wave-instruction linearly (base + 16 B * lane), so each lane fetches the
 // (row, chunk) that the image places at its linear position.
 // No VGPR staging; rows must be in bounds (callers guarantee S % tile == 0).
+// Instruction i of a lane covers image bytes i * NWV KiB further on: exactly RSTEP more rows, same
+// chunk and same XOR swizzle (the swizzle depends on row bits the step does not touch), so one
+// lane offset plus a wave-uniform row step addresses every instruction (1 VGPR instead of NI).
 template <typename T, int D, int ROWS, int NWV = 4>
 struct GStage {
   static constexpr int CH = D / 8;
   static constexpr int NI = ROWS * CH / (NWV * 64);
+  static constexpr int RSTEP = NWV * 1024 / (D * 16) * 8;
   static_assert(NI * NWV * 64 == ROWS * CH, "tile must split evenly over the block");
-  int off[NI];  // element offset of this lane's source chunk relative to the tile's first row
+  static_assert(RSTEP % 16 == 0, "row step must keep the swizzle");
+  int off0;  // element offset of this lane's first source chunk relative to the tile's first row
+  long step;  // elements between consecutive instructions' source rows (RSTEP rows)
   __device__ __forceinline__ void init(long ld) {
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      int row, ch;
-      lay_inverse<D>(((i * NWV + wid) * 64 + lane) * 16, row, ch);
-      off[i] = row * (int)ld + ch * 8;
-    }
+    int row, ch;
+    lay_inverse<D>((wid * 64 + lane) * 16, row, ch);
+    off0 = row * (int)ld + ch * 8;
+    step = (long)RSTEP * ld;
   }
   __device__ __forceinline__ void issue(const T* g, T* tile) const {
     const int wid = threadIdx.x >> 6;
 #pragma unroll
     for (int i = 0; i < NI; ++i)
-      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(g + off[i]),
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(g + i * step + off0),
                                        (__attribute__((address_space(3))) void*)(tile + (i * NWV + wid) * 512), 16, 0,
                                        0);
   }
