@@ -4,7 +4,10 @@
 Builds the bench model (default Llama-2-7B-shape, bf16, random init) on one GPU, runs a
 training step so the AdamW moments are populated, then measures for each format:
 
-* vanilla sync:   ``save_ckpt_vanilla`` until the file + .md5 are on disk (reference behaviour);
+* vanilla sync:   ``save_ckpt_vanilla`` until it returns: the archive and its ``.md5parts`` are
+                  durable (``vanilla_save_s``); the reference's whole-file ``.md5`` sidecar follows
+                  from a background digest (``vanilla_md5_sidecar_s``, measured from the same start;
+                  ``PYRECOVER_DEFER_MD5=0`` makes the save itself wait for it);
 * vanilla async:  the training-visible stall (snapshot staged, writer launched) and the
                   background completion time, with a training step running in between;
 * sharded:        ``save_ckpt_distributed`` (dcp-compatible directory) sync;
@@ -42,7 +45,7 @@ def main():
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from pyrecover_amd.ckpt import core, fastload
     from pyrecover_amd.ckpt.sharded import load_ckpt_distributed, save_ckpt_distributed
-    from pyrecover_amd.ckpt.vanilla import load_ckpt_vanilla, save_ckpt_vanilla
+    from pyrecover_amd.ckpt.vanilla import load_ckpt_vanilla, save_ckpt_vanilla, verify_checkpoint
     from pyrecover_amd.config import get_preset
     from pyrecover_amd.models.llama import Transformer
     from pyrecover_amd.optim.adamw import FlatAdamW
@@ -105,6 +108,10 @@ def main():
         save_ckpt_vanilla(model, opt, sched, None, 2, 1, p, max_keep=0, verify=args.verify)
         out["vanilla_save_s"] = round(time.perf_counter() - t0, 3)
         out["vanilla_write"] = _wstats(core)
+        if args.verify:  # the reference's whole-file .md5 sidecar lands from a background digest
+            core.flush_all()
+            out["vanilla_md5_sidecar_s"] = round(time.perf_counter() - t0, 3)
+            out["vanilla_md5_sidecar_ok"] = verify_checkpoint(p)[0]
         out["vanilla_file_gib"] = round(os.path.getsize(p) / 2**30, 3)
         del model, opt
         torch.cuda.empty_cache()

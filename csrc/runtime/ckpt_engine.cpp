@@ -29,7 +29,7 @@ void register_ckpt_engine(py::module& m) {
       .def("sync_stage", &CkptEngine::sync_stage, py::call_guard<py::gil_scoped_release>())
       .def("staged_complete", &CkptEngine::staged_complete)
       .def("write_items",
-           [](CkptEngine& e, const std::string& path, py::list items, bool md5, bool fsync) {
+           [](CkptEngine& e, const std::string& path, py::list items, bool md5, bool fsync, bool defer_md5) {
              // items: [("raw", ptr, nbytes) | ("zip", [(name, ptr, nbytes), ...])]
              std::vector<Item> v;
              for (auto h : items) {
@@ -50,9 +50,12 @@ void register_ckpt_engine(py::module& m) {
                }
                v.push_back(std::move(it));
              }
-             e.write_items(path, std::move(v), md5, fsync);
-           })
+             e.write_items(path, std::move(v), md5, fsync, defer_md5);
+           },
+           py::arg("path"), py::arg("items"), py::arg("md5"), py::arg("fsync"), py::arg("defer_md5") = false)
       .def("busy", &CkptEngine::busy)
+      .def("flush", &CkptEngine::flush, py::call_guard<py::gil_scoped_release>())
+      .def("md5_pending", &CkptEngine::md5_pending)
       .def("wait", [](CkptEngine& e) {
         JobResult r;
         {
@@ -79,6 +82,7 @@ void register_ckpt_engine(py::module& m) {
         d["records"] = recs;
         d["seg_bytes"] = r.seg_bytes;
         d["seg_md5"] = r.seg_md5;
+        d["md5_deferred"] = r.md5_deferred;
         return d;
       });
   py::class_<Reader>(m, "CkptReader")

@@ -11,6 +11,7 @@ makes the compute stream wait for the snapshot before the optimizer mutates para
 """
 from __future__ import annotations
 
+import atexit
 import logging
 import os
 import random
@@ -216,10 +217,14 @@ class Checkpointer:
             self.engine.sync_stage()
 
     # -- writing -------------------------------------------------------------------------
-    def write(self, path: str, items, md5: bool, fsync: bool, keepalive, on_done: Optional[Callable] = None) -> "Job":
+    def write(self, path: str, items, md5: bool, fsync: bool, keepalive, on_done: Optional[Callable] = None,
+              defer_md5: bool = False) -> "Job":
+        """defer_md5: the job completes once the archive and ``.md5parts`` are durable; the
+        reference's whole-file ``.md5`` (serial MD5) is finished in the background from the staged
+        bytes -- :func:`flush_all` (also before the pool is reused, and at exit) waits for it."""
         self.wait()
         os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
-        self.engine.write_items(str(path), items, md5, fsync)
+        self.engine.write_items(str(path), items, md5, fsync, defer_md5)
         self.pending = Job(self, str(path), keepalive, on_done, started=time.perf_counter())
         _maybe_inject_fault("during_write", path)
         return self.pending
@@ -237,6 +242,13 @@ class Checkpointer:
         """Collect a finished background write without blocking (records its duration)."""
         if self.pending is not None and not self.engine.busy():
             self.wait()
+
+    def flush(self):
+        """Wait for the in-flight write and any deferred whole-file ``.md5`` digest."""
+        self.wait()
+        err = self.engine.flush()
+        if err:
+            raise RuntimeError(f"deferred checkpoint md5 failed: {err}")
 
 
 # Background-write durations feed the time-aware stop: the FINAL checkpoint is written
@@ -286,6 +298,22 @@ def inflight_remaining(estimate: float) -> float:
         if j is not None and j.result is None and c.engine.busy():
             rem = max(rem, estimate - (now - j.started))
     return max(rem, 0.0)
+
+
+def flush_all():
+    """wait_all() plus the deferred whole-file ``.md5`` digests (their sidecars exist afterwards)."""
+    for c in list(Checkpointer._instances.values()):
+        c.flush()
+
+
+def _flush_at_exit():
+    try:
+        flush_all()
+    except Exception as e:  # noqa: BLE001 - interpreter shutdown: report, do not raise
+        logger.warning(f"checkpoint flush at exit: {e}")
+
+
+atexit.register(_flush_at_exit)
 
 
 def wait_all():

@@ -410,10 +410,11 @@ def train(args):
         if args.profile and args.profile_step_end == train_step:
             _profiler_stop()
 
-    # drain background checkpoint writes before reporting
+    # drain background checkpoint writes (and deferred .md5 digests) before reporting
     t0 = time.perf_counter()
     ckcore.wait_all()
     finalize_pending()
+    ckcore.flush_all()
     total_checkpoint_store_time += time.perf_counter() - t0
     total_training_time = time.perf_counter() - training_start_time
     if csv_file is not None:

@@ -2,8 +2,9 @@
 // (device -1: no HIP calls), built with -fsanitize=address,undefined or -fsanitize=thread by
 // tests/test_native_sanitizers.py. Exercises: pool reserve, parallel host staging, the writer
 // threads (zip records + raw blob in one file, CRC32 pieces, parallel segment writes + MD5s,
-// whole-file MD5, tmp+rename, .md5 sidecar), the parallel Reader (O_DIRECT and buffered), the
-// error paths, and back-to-back jobs reusing the pool.
+// whole-file MD5, tmp+rename, .md5 sidecar), the deferred whole-file digest (third round: the job
+// returns before the `.md5` exists; the caller's raw bytes are freed before flush()), the parallel
+// Reader (O_DIRECT and buffered), the error paths, and back-to-back jobs reusing the pool.
 // usage: ckpt_engine_selftest <out_dir>   -> exit 0 on success; writes <out_dir>/t.bin
 #include "runtime/ckpt_engine.h"
 
@@ -43,7 +44,7 @@ int main(int argc, char** argv) {
 
   CkptEngine eng(-1);
   eng.reserve(64u << 20);
-  for (int round = 0; round < 2; ++round) {  // the pool is reused by the second job
+  for (int round = 0; round < 3; ++round) {  // the pool is reused by later jobs; round 2 defers the .md5
     std::vector<std::pair<uintptr_t, uint64_t>> regions;
     for (auto& v : src) regions.push_back({(uintptr_t)v.data(), v.size()});
     const auto offs = eng.stage(regions, nullptr);
@@ -54,14 +55,24 @@ int main(int argc, char** argv) {
     Item zip;
     for (size_t i = 0; i < src.size(); ++i)
       zip.records.push_back({"archive/data/" + std::to_string(i), pool + offs[i], src[i].size()});
+    const bool defer = round == 2;
+    std::vector<uint8_t>* raw_copy = new std::vector<uint8_t>(raw);  // caller-owned, freed after wait()
     Item rawi;
     rawi.raw = true;
-    rawi.ptr = (uintptr_t)raw.data();
-    rawi.n = raw.size();
+    rawi.ptr = (uintptr_t)raw_copy->data();
+    rawi.n = raw_copy->size();
     const std::string path = dir + "/t.bin";
-    eng.write_items(path, {zip, rawi}, /*md5=*/true, /*fsync=*/round == 0);
-    const JobResult r = eng.wait();
+    eng.write_items(path, {zip, rawi}, /*md5=*/true, /*fsync=*/round == 0, defer);
+    JobResult r = eng.wait();
+    std::memset(raw_copy->data(), 0xEE, raw_copy->size());
+    delete raw_copy;
     REQUIRE(r.ok);
+    REQUIRE(r.md5_deferred == defer);
+    if (defer) {
+      REQUIRE(eng.flush().empty());
+      r.md5 = slurp(path + ".md5");
+      REQUIRE(r.md5.size() == 32);
+    }
     REQUIRE(r.items.size() == 2);
     const std::string file = slurp(path);
     REQUIRE(file.size() == r.bytes);

@@ -15,7 +15,7 @@ import torch
 import torch.multiprocessing as mp
 
 from pyrecover_amd import _ext
-from pyrecover_amd.ckpt import fastload
+from pyrecover_amd.ckpt import core, fastload
 from pyrecover_amd.ckpt.sharded import MANIFEST, load_ckpt_distributed, save_ckpt_distributed
 from pyrecover_amd.ckpt.vanilla import load_ckpt_vanilla, save_ckpt_vanilla
 from pyrecover_amd.config import get_preset
@@ -77,6 +77,10 @@ def test_md5parts_sidecar_and_corruption(tmp_path):
     p = str(tmp_path / "ckpt_1.pt")
     save_ckpt_vanilla(m, opt, sched, None, 1, 1, p, max_keep=0, verify=True)
     data = open(p, "rb").read()
+    # the whole-file .md5 is a deferred background digest: it exists once flushed (and before
+    # the staging pool is reused / at exit); .md5parts exists when the save returns
+    assert os.path.exists(p + ".md5parts")
+    core.flush_all()
     assert open(p + ".md5").read() == hashlib.md5(data).hexdigest()
     seg, total, md5s = fastload.read_md5parts(p)
     assert total == len(data) and seg == _ext.native().MD5PARTS_SEGMENT_BYTES
