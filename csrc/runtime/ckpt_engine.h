@@ -332,7 +332,6 @@ class CkptEngine {
   // Ensure the pinned pool holds at least nbytes (must not be called while a job runs).
   void reserve(uint64_t nbytes) {
     wait_writer();
-    flush();
     if (nbytes <= pool_size_) return;
     release_chunks();
     free_pool();
@@ -354,7 +353,6 @@ class CkptEngine {
   // caller's compute stream; ignored in CPU mode).
   std::vector<uint64_t> stage(const std::vector<std::pair<uintptr_t, uint64_t>>& regions, hipStream_t cur) {
     wait_writer();  // the pool is reused: the previous archive must be fully written
-    flush();        // ... and its deferred whole-file digest computed
     release_chunks();
     uint64_t total = 0;
     std::vector<uint64_t> offs;
@@ -420,9 +418,8 @@ class CkptEngine {
   // Start writing a zip archive on the background thread. Records point into the pinned pool
   // (waited per chunk) or into caller-owned host memory kept alive until wait().
   // defer_md5: the job completes once the archive and its `.md5parts` are durable; the reference's
-  // whole-file `.md5` (serial MD5, ~1 GB/s: 38 s at 7B) is finished by a background thread from
-  // the staged bytes and appears atomically later -- flush() (also run before the pool is reused
-  // and at destruction) waits for it.
+  // whole-file `.md5` (serial MD5, ~0.9 GB/s: ~45 s at 7B) is computed by a background thread that
+  // re-reads the file, and appears atomically later -- flush() (also run at destruction) waits.
   void write_items(const std::string& path, std::vector<Item> items, bool want_md5, bool do_fsync,
                    bool defer_md5 = false) {
     wait_writer();
@@ -460,7 +457,12 @@ class CkptEngine {
 
   // Wait for a deferred whole-file digest; returns its error ("" if none / nothing pending).
   std::string flush() {
-    if (md5_th_.joinable()) md5_th_.join();
+    std::vector<std::thread> th;
+    {
+      std::lock_guard<std::mutex> g(md5_th_mu_);
+      th.swap(md5_th_);
+    }
+    for (auto& t : th) t.join();
     std::lock_guard<std::mutex> g(mu_);
     std::string e;
     e.swap(md5_error_);
@@ -468,7 +470,7 @@ class CkptEngine {
   }
   bool md5_pending() {
     std::lock_guard<std::mutex> g(mu_);
-    return md5_running_;
+    return md5_running_ > 0;
   }
 
  private:
@@ -824,48 +826,39 @@ class CkptEngine {
       if (whole_md5 && !deferred) write_sidecar(path + ".md5", r.md5, do_fsync);
       write_sidecar(path + ".md5parts", md5parts_text(r.seg_bytes, total, r.seg_md5), do_fsync);
     }
-    if (deferred) start_deferred_md5(path, pieces, owned, do_fsync, r);
+    if (deferred) start_deferred_md5(path, do_fsync, r);
   }
 
-  // The deferred digest reads the staged pool (kept until flush(): stage() and reserve() call it)
-  // and the zip headers (moved in); any other caller-owned bytes (small pickles, CPU tensors) are
-  // copied here, because the caller releases them when the job completes.
-  void start_deferred_md5(const std::string& path, const std::vector<Piece>& pieces,
-                          std::deque<std::vector<uint8_t>>& owned, bool do_fsync, JobResult& r) {
-    auto own = std::make_shared<std::deque<std::vector<uint8_t>>>(std::move(owned));
-    std::vector<Piece> pcs = pieces;
-    const uintptr_t lo = (uintptr_t)pool_, hi = lo + pool_size_;
-    for (auto& pc : pcs) {
-      const uintptr_t a = (uintptr_t)pc.p;
-      bool held = a >= lo && a + pc.n <= hi;
-      for (auto& v : *own)
-        if (!held && a >= (uintptr_t)v.data() && a + pc.n <= (uintptr_t)v.data() + v.size()) held = true;
-      if (!held) {
-        own->emplace_back(pc.p, pc.p + pc.n);
-        pc.p = own->back().data();
-      }
-    }
-    if (md5_th_.joinable()) md5_th_.join();
+  // The deferred digest re-reads the finished FILE (streaming, double-buffered preads; the serial
+  // MD5 at ~1 GB/s, not the read, is its speed limit), so it holds no staging memory: the next
+  // snapshot can reuse the pool at once, and several digests may be in flight (flush() joins all).
+  void start_deferred_md5(const std::string& path, bool do_fsync, JobResult& r) {
     {
       std::lock_guard<std::mutex> g(mu_);
-      md5_running_ = true;
+      ++md5_running_;
     }
     r.md5_deferred = true;
-    md5_th_ = std::thread([this, path, pcs = std::move(pcs), own, do_fsync] {
+    std::lock_guard<std::mutex> g(md5_th_mu_);
+    md5_th_.emplace_back([this, path, do_fsync] {
       std::string err;
       try {
-        EVP_MD_CTX* ctx = EVP_MD_CTX_new();
-        EVP_DigestInit_ex(ctx, EVP_md5(), nullptr);
-        for (auto& pc : pcs) EVP_DigestUpdate(ctx, pc.p, pc.n);
-        const std::string md5 = digest_hex(ctx);
-        EVP_MD_CTX_free(ctx);
+        const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+        if (fd < 0) throw std::runtime_error("ckpt_engine: deferred md5: cannot open " + path);
+        std::string md5;
+        try {
+          md5 = md5_fd(fd);
+        } catch (...) {
+          ::close(fd);
+          throw;
+        }
+        ::close(fd);
         write_sidecar(path + ".md5", md5, do_fsync);
       } catch (const std::exception& e) {
         err = e.what();
       }
-      std::lock_guard<std::mutex> g(mu_);
+      std::lock_guard<std::mutex> g2(mu_);
       if (!err.empty()) md5_error_ = err;
-      md5_running_ = false;
+      --md5_running_;
     });
   }
 
@@ -887,10 +880,11 @@ class CkptEngine {
   uint64_t staged_bytes_ = 0;
   std::vector<Chunk> chunks_;
   std::thread writer_;
-  std::thread md5_th_;  // deferred whole-file digest
+  std::vector<std::thread> md5_th_;  // deferred whole-file digests
+  std::mutex md5_th_mu_;
   std::mutex mu_;
   bool running_ = false;
-  bool md5_running_ = false;
+  int md5_running_ = 0;
   std::string md5_error_;
   JobResult result_;
 };

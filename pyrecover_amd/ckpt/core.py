@@ -220,8 +220,8 @@ class Checkpointer:
     def write(self, path: str, items, md5: bool, fsync: bool, keepalive, on_done: Optional[Callable] = None,
               defer_md5: bool = False) -> "Job":
         """defer_md5: the job completes once the archive and ``.md5parts`` are durable; the
-        reference's whole-file ``.md5`` (serial MD5) is finished in the background from the staged
-        bytes -- :func:`flush_all` (also before the pool is reused, and at exit) waits for it."""
+        reference's whole-file ``.md5`` (serial MD5) is computed in the background by re-reading
+        the file (no staging memory held) -- :func:`flush_all` (also at exit) waits for it."""
         self.wait()
         os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
         self.engine.write_items(str(path), items, md5, fsync, defer_md5)

@@ -60,8 +60,8 @@ def save_ckpt_vanilla(model, optimizer, lr_scheduler=None, sampler=None, step: i
             logger.info(f"checkpoint {checkpoint_path}: {res['bytes'] / 2**30:.2f} GiB in {res['seconds']:.2f}s" + md5)
 
         # The archive and its .md5parts (parallel per-segment MD5s, what our loader verifies) are
-        # durable when the job completes; the reference's whole-file .md5 (serial MD5 at ~1 GB/s,
-        # 38 s at 7B) follows from the staged bytes in the background unless PYRECOVER_DEFER_MD5=0.
+        # durable when the job completes; the reference's whole-file .md5 (serial MD5 at ~0.9 GB/s,
+        # ~45 s at 7B) follows from a background re-read of the file unless PYRECOVER_DEFER_MD5=0.
         defer = verify and os.environ.get("PYRECOVER_DEFER_MD5", "1") != "0"
         ck.write(str(checkpoint_path), [("zip", records)], verify, fsync, (staged, keep), done, defer_md5=defer)
         if not async_save:
