@@ -56,6 +56,7 @@ void register_ckpt_engine(py::module& m) {
       .def("busy", &CkptEngine::busy)
       .def("flush", &CkptEngine::flush, py::call_guard<py::gil_scoped_release>())
       .def("md5_pending", &CkptEngine::md5_pending)
+      .def("abandon_md5", &CkptEngine::abandon_md5)
       .def("wait", [](CkptEngine& e) {
         JobResult r;
         {

@@ -468,6 +468,14 @@ class CkptEngine {
     e.swap(md5_error_);
     return e;
   }
+  // Stop waiting for deferred digests (a job about to be killed by its wall-clock limit): they
+  // keep running until the process exits; a digest cut short leaves no `.md5` (the `.md5parts`
+  // written with the archive still verify it).
+  void abandon_md5() {
+    std::lock_guard<std::mutex> g(md5_th_mu_);
+    for (auto& t : md5_th_) t.detach();
+    md5_th_.clear();
+  }
   bool md5_pending() {
     std::lock_guard<std::mutex> g(mu_);
     return md5_running_ > 0;

@@ -300,13 +300,38 @@ def inflight_remaining(estimate: float) -> float:
     return max(rem, 0.0)
 
 
-def flush_all():
-    """wait_all() plus the deferred whole-file ``.md5`` digests (their sidecars exist afterwards)."""
+def flush_all(deadline: Optional[float] = None) -> bool:
+    """wait_all() plus the deferred whole-file ``.md5`` digests (their sidecars exist afterwards).
+    With ``deadline`` (a ``time.time()`` value) digests still running then are abandoned instead
+    (:func:`abandon_deferred_md5`); returns False in that case."""
+    if deadline is not None:
+        wait_all()
+        while any(c.engine.md5_pending() for c in Checkpointer._instances.values()):
+            if time.time() >= deadline:
+                abandon_deferred_md5()
+                return False
+            time.sleep(0.05)
     for c in list(Checkpointer._instances.values()):
         c.flush()
+    return True
+
+
+_FLUSH_AT_EXIT = [True]
+
+
+def abandon_deferred_md5():
+    """Do not wait for deferred ``.md5`` digests, now or at exit (the time-aware final checkpoint:
+    the job's wall-clock limit is near). A digest cut short leaves no ``.md5``; the ``.md5parts``
+    written with the archive still verify the resume."""
+    _FLUSH_AT_EXIT[0] = False
+    for c in list(Checkpointer._instances.values()):
+        c.wait()
+        c.engine.abandon_md5()
 
 
 def _flush_at_exit():
+    if not _FLUSH_AT_EXIT[0]:
+        return
     try:
         flush_all()
     except Exception as e:  # noqa: BLE001 - interpreter shutdown: report, do not raise

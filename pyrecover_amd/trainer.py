@@ -276,6 +276,7 @@ def train(args):
 
     train_dl_iterator = iter(train_dl)
     should_stop = False
+    stopped_for_time = False
     stop_flag = torch.zeros(1, dtype=torch.int32, device=device)
     log_rank0("Starting training!")
     loss = None
@@ -401,6 +402,7 @@ def train(args):
             _, store_time = do_save(train_step, epoch, final=True)
             total_checkpoint_store_time += store_time
             log_rank0(f"[TIME CHECK] Final checkpoint store completed in {store_time:.2f} seconds")
+            stopped_for_time = True
             if args.resubmit != "none":
                 resub.maybe_resubmit(rank)
             break
@@ -410,11 +412,19 @@ def train(args):
         if args.profile and args.profile_step_end == train_step:
             _profiler_stop()
 
-    # drain background checkpoint writes (and deferred .md5 digests) before reporting
+    # drain background checkpoint writes (and deferred .md5 digests) before reporting; after a
+    # time-aware stop the digests get only the time left before the wall-clock limit (minus a
+    # margin; 60 s after a signal) -- one cut short leaves no .md5, and .md5parts verify the resume
     t0 = time.perf_counter()
     ckcore.wait_all()
     finalize_pending()
-    ckcore.flush_all()
+    if stopped_for_time:
+        end = getattr(stopper, "end_time", None)
+        deadline = max((end - 10.0) if end else time.time() + 60.0, time.time() + 2.0)
+        if not ckcore.flush_all(deadline=deadline):
+            log_rank0("[TIME CHECK] deferred .md5 digest abandoned at the wall-clock limit (.md5parts verify)")
+    else:
+        ckcore.flush_all()
     total_checkpoint_store_time += time.perf_counter() - t0
     total_training_time = time.perf_counter() - training_start_time
     if csv_file is not None:
