@@ -346,11 +346,14 @@ def test_rope_t_matches_rope_exactly(cuda):
     assert torch.equal(xT, ref.t().contiguous())
 
 
-@pytest.mark.parametrize("rows,cols", [(64, 64), (192, 320), (4096, 128)])
+@pytest.mark.parametrize("rows,cols", [(64, 64), (192, 320), (4096, 128), (128, 512)])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-def test_adamw_t_matches_flat_adamw_plus_transpose(cuda, rows, cols, dtype):
+@pytest.mark.parametrize("strip", ["1", "4"])
+def test_adamw_t_matches_flat_adamw_plus_transpose(cuda, monkeypatch, strip, rows, cols, dtype):
     """Fused AdamW + transposed-shadow write == flat AdamW followed by transpose2d, bit for bit
-    (incl. device-side grad scale and hyper-parameters)."""
+    (incl. device-side grad scale and hyper-parameters), for the one-tile and the strip kernel
+    (PRA_ADAMW_T_STRIP; 4 falls back to 2 / 1 tiles per block when cols/64 is not divisible)."""
+    monkeypatch.setenv("PRA_ADAMW_T_STRIP", strip)
     C = _ext.native()
     torch.manual_seed(rows + cols)
     p = torch.randn(rows, cols, device=cuda).to(dtype)
