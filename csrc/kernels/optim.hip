@@ -252,11 +252,12 @@ hipError_t pra_adamw_t(int dtype, void* p, const void* g, void* m, void* v, void
                        float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt, float gscale,
                        const float* gscale_dev, const float* hyper_dev, hipStream_t s) {
   if (rows % 64 || cols % 64 || rows <= 0 || cols <= 0) return hipErrorInvalidValue;
-  // PRA_ADAMW_T_STRIP (read per call): tiles per block of the strip kernel (1 = one-tile kernel).
-  // Default 4: one 7B optimizer step 22.7 -> 21.3 ms in isolation, bit-identical results
-  // (tools/adamw_bench.py, profiles/adamw_t_strip_ab_r2.log)
+  // PRA_ADAMW_T_STRIP (read per call): tiles per block of the strip kernel (1 = one-tile kernel,
+  // the default). In isolation 4 tiles per block is faster (7B optimizer step 22.7 -> 21.3 ms,
+  // bit-identical), but overlapped with the backward GEMMs on the side stream its long-lived blocks
+  // cost the step more (1069.6 vs 1074.5 ms, same box; profiles/adamw_t_strip_ab_r2.log).
   const char* e = getenv("PRA_ADAMW_T_STRIP");
-  int nt = e ? atoi(e) : 4;
+  int nt = e ? atoi(e) : 1;
   while (nt > 1 && (cols / 64) % nt) nt /= 2;
 #define PRA_ADAMW_T_LAUNCH(NT)                                                                                  \
   PRA_DISPATCH_16BIT(dtype, T,                                                                                  \
