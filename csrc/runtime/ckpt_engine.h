@@ -463,9 +463,9 @@ class CkptEngine {
       th.swap(md5_th_);
     }
     for (auto& t : th) t.join();
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<std::mutex> g(md5st_->mu);
     std::string e;
-    e.swap(md5_error_);
+    e.swap(md5st_->error);
     return e;
   }
   // Stop waiting for deferred digests (a job about to be killed by its wall-clock limit): they
@@ -477,8 +477,8 @@ class CkptEngine {
     md5_th_.clear();
   }
   bool md5_pending() {
-    std::lock_guard<std::mutex> g(mu_);
-    return md5_running_ > 0;
+    std::lock_guard<std::mutex> g(md5st_->mu);
+    return md5st_->running > 0;
   }
 
  private:
@@ -841,13 +841,14 @@ class CkptEngine {
   // MD5 at ~1 GB/s, not the read, is its speed limit), so it holds no staging memory: the next
   // snapshot can reuse the pool at once, and several digests may be in flight (flush() joins all).
   void start_deferred_md5(const std::string& path, bool do_fsync, JobResult& r) {
+    std::shared_ptr<Md5State> st = md5st_;  // shared: an abandoned (detached) digest outlives nothing it uses
     {
-      std::lock_guard<std::mutex> g(mu_);
-      ++md5_running_;
+      std::lock_guard<std::mutex> g(st->mu);
+      ++st->running;
     }
     r.md5_deferred = true;
     std::lock_guard<std::mutex> g(md5_th_mu_);
-    md5_th_.emplace_back([this, path, do_fsync] {
+    md5_th_.emplace_back([st, path, do_fsync] {
       std::string err;
       try {
         const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
@@ -864,9 +865,9 @@ class CkptEngine {
       } catch (const std::exception& e) {
         err = e.what();
       }
-      std::lock_guard<std::mutex> g2(mu_);
-      if (!err.empty()) md5_error_ = err;
-      --md5_running_;
+      std::lock_guard<std::mutex> g2(st->mu);
+      if (!err.empty()) st->error = err;
+      --st->running;
     });
   }
 
@@ -888,12 +889,16 @@ class CkptEngine {
   uint64_t staged_bytes_ = 0;
   std::vector<Chunk> chunks_;
   std::thread writer_;
+  struct Md5State {
+    std::mutex mu;
+    int running = 0;
+    std::string error;
+  };
   std::vector<std::thread> md5_th_;  // deferred whole-file digests
   std::mutex md5_th_mu_;
+  std::shared_ptr<Md5State> md5st_ = std::make_shared<Md5State>();
   std::mutex mu_;
   bool running_ = false;
-  int md5_running_ = 0;
-  std::string md5_error_;
   JobResult result_;
 };
 

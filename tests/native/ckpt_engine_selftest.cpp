@@ -103,6 +103,22 @@ int main(int argc, char** argv) {
     const ReadResult bad_rd = rd.read(path, {{r.bytes - 4, 64, (uintptr_t)back[0].data()}}, {}, 2, false);
     REQUIRE(!bad_rd.ok && !bad_rd.error.empty());
   }
+  // an abandoned deferred digest outlives its engine (time-aware stop at the wall-clock limit):
+  // it must touch nothing the engine owned, and still write the sidecar
+  {
+    auto* e2 = new CkptEngine(-1);
+    e2->reserve(1u << 20);
+    const auto o2 = e2->stage({{(uintptr_t)src[0].data(), src[0].size()}}, nullptr);
+    Item z2;
+    z2.records.push_back({"archive/data/0", e2->pool_ptr() + o2[0], src[0].size()});
+    const std::string p2 = dir + "/abandoned.bin";
+    e2->write_items(p2, {z2}, /*md5=*/true, /*fsync=*/false, /*defer_md5=*/true);
+    REQUIRE(e2->wait().ok);
+    e2->abandon_md5();
+    delete e2;
+    for (int i = 0; i < 200 && access((p2 + ".md5").c_str(), F_OK) != 0; ++i) usleep(10000);
+    REQUIRE(slurp(p2 + ".md5") == md5_file(p2));
+  }
   // error path: unwritable destination -> ok=false, message, nothing left behind
   eng.write_items(dir + "/no/such/dir/x.bin", {}, true, false);
   const JobResult bad = eng.wait();
