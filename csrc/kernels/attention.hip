@@ -393,7 +393,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_kernel(const T* __restrict__ Q
 // iteration t and written into the slot tile t-1 vacated, one barrier per tile. In causal mode a
 // wave's only diagonal tile is its last one.
 // ======================================================================================
-template <typename T, int D, bool CAUSAL, int NW>
+template <typename T, int D, bool CAUSAL, int NW, bool BAL = false>
 __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const T* __restrict__ Q, const T* __restrict__ K,
                                                            const T* __restrict__ V, T* __restrict__ O,
                                                            float* __restrict__ LSE, int S, int Hq, int Hkv, long ldq,
@@ -494,8 +494,14 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const T* __restrict__
       const T* Vt = s_cur + TILE;
       auto iter = [&](auto next_c, auto diag_c) {
         constexpr bool NEXT = decltype(next_c)::value, DIAG = decltype(diag_c)::value;
-        constexpr int RA = NKS, EA = 32 / RA;  // phase A: regions / softmax elements per region
+        // BAL: phase A exponentiates 24 of tile t's 32 scores per lane (all of c0, the first half of
+        // c1) and phase B the last 8 (c1[8..15], only read by the P.V k-step of its second half)
+        // in its first half, so both phases carry about the same VALU per MFMA; otherwise phase A
+        // takes all 32 exponentials and phase B only the row max.
+        constexpr int NEA = BAL ? 24 : 32;
+        constexpr int RA = NKS, EA = NEA / RA;  // phase A: regions / softmax elements per region
         constexpr int RB = 2 * NDB, EB = 32 / RB;
+        constexpr int EBX = BAL ? (32 - NEA) / (RB / 2) : 0;  // phase B exponentials per region
         f32x16 n0 = f32x16{}, n1 = f32x16{};
         float rs = 0.f, mx = -INFINITY;
         auto expo = [&](int e) {  // element e of the 32 scores of tile t
@@ -526,8 +532,8 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const T* __restrict__
           a1 = b1;
           __builtin_amdgcn_sched_barrier(0);
         }
-        l_i += half_sum(rs);
-        const V8<T> p[4] = {pack8<T>(c0, 0), pack8<T>(c0, 1), pack8<T>(c1, 0), pack8<T>(c1, 1)};
+        if (!BAL) l_i += half_sum(rs);
+        V8<T> p[4] = {pack8<T>(c0, 0), pack8<T>(c0, 1), pack8<T>(c1, 0), pack8<T>(c1, 1)};
         if (NEXT && DIAG) mask(n0, n1, (t + 1) * KT);
         // phase B: O^T += V_t^T P_t | row max of tile t+1
         V8<T> vc[2] = {lo.tr(Vt, 0, 0), lo.tr(Vt, (1 / NDB) * 16, 1 % NDB)};
@@ -542,6 +548,16 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const T* __restrict__
           const int s0 = 2 * k, s1 = s0 + 1;
           o[s0 % NDB] = mfma(vc[0], p[s0 / NDB], o[s0 % NDB]);
           o[s1 % NDB] = mfma(vc[1], p[s1 / NDB], o[s1 % NDB]);
+          if constexpr (BAL) {
+            if (k < RB / 2) {
+#pragma unroll
+              for (int e = 0; e < EBX; ++e) expo(NEA + k * EBX + e);
+              if (k == RB / 2 - 1) {  // P of keys 48..63 complete (first read in region 3 RB / 4)
+                p[3] = pack8<T>(c1, 1);
+                l_i += half_sum(rs);
+              }
+            }
+          }
           if (NEXT) {
 #pragma unroll
             for (int e = 0; e < EB; ++e) {
@@ -1214,8 +1230,15 @@ hipError_t attn_fwd_t(const void* q, const void* k, const void* v, void* o, floa
   // 0 = exact rescale at every growth.
   const char* ft = getenv("PRA_FWD_THR");
   const float thr = ft ? (float)atof(ft) : 8.f;
+  // PRA_FWD_BAL (read per call, default 1): exponentials split between the two phases of the
+  // pipelined kernel (B16 S2048 H32 fwd 0.747 -> 0.734 ms, B1 S8192 H32/8 0.520 -> 0.508 ms)
+  const char* fb = getenv("PRA_FWD_BAL");
+  const bool bal = fb ? atoi(fb) != 0 : true;
 #define LAUNCH(DD, CC)                                                                                        \
-  if (pipe)                                                                                                   \
+  if (pipe && bal)                                                                                            \
+    hipLaunchKernelGGL((fwd_p_kernel<T, DD, CC, NW, true>), grid, block, 0, st, (const T*)q, (const T*)k,   \
+                       (const T*)v, (T*)o, lse, S, Hq, Hkv, ldq, ldk, ldv, ldo, sl2, thr);                  \
+  else if (pipe)                                                                                              \
     hipLaunchKernelGGL((fwd_p_kernel<T, DD, CC, NW>), grid, block, 0, st, (const T*)q, (const T*)k,         \
                        (const T*)v, (T*)o, lse, S, Hq, Hkv, ldq, ldk, ldv, ldo, sl2, thr);                  \
   else                                                                                                        \

@@ -188,10 +188,11 @@ def _qkv(cuda, B, S, Hq, Hkv, D, seed=0, scale=1.0):
 @pytest.mark.parametrize("B,S,Hq,Hkv,D", [(1, 256, 4, 4, 128), (2, 512, 8, 2, 128), (1, 384, 4, 1, 64),
                                           (1, 128, 2, 2, 64), (1, 192, 4, 2, 128)])
 @pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("pipe", ["0", "1"])
+@pytest.mark.parametrize("pipe", ["0", "1", "bal"])
 def test_attention_fwd(cuda, monkeypatch, pipe, B, S, Hq, Hkv, D, causal):
-    """Both forward kernels (PRA_FWD_PIPE: fwd_kernel / cross-tile pipelined fwd_p_kernel)."""
-    monkeypatch.setenv("PRA_FWD_PIPE", pipe)
+    """Every forward kernel (PRA_FWD_PIPE: fwd_kernel / cross-tile pipelined fwd_p_kernel, and the
+    pipelined kernel with its exponentials split between its phases, PRA_FWD_BAL)."""
+    _fwd_variant(monkeypatch, pipe)
     C = _ext.native()
     _, q, k, v = _qkv(cuda, B, S, Hq, Hkv, D)
     scale = 1 / math.sqrt(D)
@@ -201,12 +202,17 @@ def test_attention_fwd(cuda, monkeypatch, pipe, B, S, Hq, Hkv, D, causal):
     assert (lse - lse_ref).abs().max().item() < 1e-3
 
 
-@pytest.mark.parametrize("pipe", ["0", "1"])
+def _fwd_variant(monkeypatch, pipe):
+    monkeypatch.setenv("PRA_FWD_PIPE", "1" if pipe == "bal" else pipe)
+    monkeypatch.setenv("PRA_FWD_BAL", "1" if pipe == "bal" else "0")
+
+
+@pytest.mark.parametrize("pipe", ["0", "1", "bal"])
 @pytest.mark.parametrize("thr", ["0", "8"])
 def test_attention_fwd_rescale_spike(cuda, monkeypatch, pipe, thr):
     """Forces the online-softmax running max to jump at a late key tile (rule 26), with the exact
     rescale (PRA_FWD_THR=0) and the default deferred threshold."""
-    monkeypatch.setenv("PRA_FWD_PIPE", pipe)
+    _fwd_variant(monkeypatch, pipe)
     monkeypatch.setenv("PRA_FWD_THR", thr)
     C = _ext.native()
     B, S, H, D = 1, 512, 2, 128
