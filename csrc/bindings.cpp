@@ -582,7 +582,7 @@ void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, con
                        lp.data_ptr<float>(), delta.data_ptr<float>(), dqp.data_ptr(), dkp.data_ptr(), dvp.data_ptr(),
                        (int)B, (int)Sp, (int)Hq, (int)Hkv, (int)D, qp.stride(1), kp.stride(1), vp.stride(1),
                        op.stride(1), dop.stride(1), dqp.stride(1), dkp.stride(1), dvp.stride(1), (float)scale,
-                       causal ? 1 : 0, (int)S, stream_of(q)),
+                       causal ? 1 : 0, (int)S, nullptr, 0, stream_of(q)),
           "attn_bwd");
     dq.copy_(dqp.narrow(1, 0, S));
     dk.copy_(dkp.narrow(1, 0, S));
@@ -590,11 +590,16 @@ void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, con
     return;
   }
   at::Tensor delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
+  // dS-materializing backward: a [B, Hq, S, S] 16-bit workspace (from the caching allocator, so
+  // every layer's backward reuses the same block) when the launcher would take that path
+  const size_t ds_bytes = pra_attn_bwd_ds_bytes((int)B, (int)S, (int)Hq, (int)Hkv, (int)D, causal ? 1 : 0);
+  at::Tensor ds_ws;
+  if (ds_bytes) ds_ws = at::empty({(int64_t)(ds_bytes / 2)}, q.options());
   check(pra_attn_bwd(dt(q), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
                      lse.data_ptr<float>(), delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
                      (int)B, (int)S, (int)Hq, (int)Hkv, (int)D, q.stride(1), k.stride(1), v.stride(1), o.stride(1),
                      dout.stride(1), dq.stride(1), dk.stride(1), dv.stride(1), (float)scale, causal ? 1 : 0, (int)S,
-                     stream_of(q)),
+                     ds_bytes ? ds_ws.data_ptr() : nullptr, ds_bytes, stream_of(q)),
         "attn_bwd");
 }
 

@@ -671,12 +671,14 @@ __global__ __launch_bounds__(256) void bwd_pre_kernel(const T* __restrict__ O, c
 // NW = 4 (128 keys, 80 KB, two blocks per CU): the constants arrive as one float per lane and are
 // broadcast with ds_bpermute (no LDS left for them).
 // ======================================================================================
-template <typename T, int D, bool CAUSAL, int NW>
+// WDS: also store dS (bf16/fp16, the exact values the dK MFMAs consume) into dS[b, hq, q, k]
+// ([S, S] per head; only tiles on or below the causal diagonal are written), for bwd_dq_ds_kernel.
+template <typename T, int D, bool CAUSAL, int NW, bool WDS = false>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
     const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V,
     const T* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
     T* __restrict__ dK, T* __restrict__ dV, int S, int Hq, int Hkv, long ldq, long ldk, long ldv,
-    long lddo, long lddk, long lddv, float scale, float scale_log2, int prio, int skv) {
+    long lddo, long lddk, long lddv, float scale, float scale_log2, int prio, int skv, T* __restrict__ dS = nullptr) {
   constexpr int KB = 32 * NW, QT = 32, NT = NW * 64;
   constexpr int NKS = D / 16, NDB = D / 32;
   constexpr int KVT = KB * D, QDT = QT * D;
@@ -796,6 +798,18 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
         }
       }
       const V8<T> p0 = pack8<T>(s, 0), p1 = pack8<T>(s, 1), d0 = pack8<T>(dp, 0), d1 = pack8<T>(dp, 1);
+      if constexpr (WDS) {
+        // column krow of rows q0 + crow(r, h2) of this head's [S, S] dS (lanes of a half-wave write
+        // 64 B): buffer stores with the lane part in one VGPR offset and the row in the scalar offset
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(dS + (long)__builtin_amdgcn_readfirstlane(b * Hq + hq) * S * S), (short)0,
+            __builtin_amdgcn_readfirstlane(S * S * 2), 0x00020000);
+        const int voff = (4 * h2 * S + krow) * 2;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (T)dp[r]), rsrc, voff,
+                                                __builtin_amdgcn_readfirstlane((q0 + crow(r, 0)) * S * 2), 0);
+      }
       V8<T> ot = lo.tr(Ds, 0, 0), qt = lo.tr(Qs, 0, 0);
 #pragma unroll
       for (int st = 0; st < 2 * NDB; ++st) {
@@ -1199,6 +1213,93 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
   store_rows16<T, NDB>(dqt, scale, dQ + ((long)b * S + qrow) * lddq + hq * D, qrow < S, h2);
 }
 
+// ======================================================================================
+// Backward dQ from a materialized dS (causal, after bwd_dkdv_kernel<..., WDS>): dQ^T = K^T dS^T.
+// Block = (b, q head, 32 NW queries), wave = 32 queries; 64-key K tiles by LDS-DMA (double buffer,
+// one __shared__ object per buffer), dS fragments loaded straight into registers one tile ahead.
+// One GEMM per key tile instead of the three of bwd_dq_kernel (S and dP are not recomputed);
+// keys past a wave's last query are masked on its diagonal tile (dS is not written there).
+// ======================================================================================
+template <typename T, int D, int NW>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_ds_kernel(const T* __restrict__ K,
+                                                                    const T* __restrict__ dS, T* __restrict__ dQ,
+                                                                    int S, int Hq, int Hkv, long ldk, long lddq,
+                                                                    float scale) {
+  constexpr int KT = 64, QT = 32 * NW;
+  constexpr int NDB = D / 32, TILE = KT * D;
+  __shared__ __attribute__((aligned(16))) T kb0[TILE];
+  __shared__ __attribute__((aligned(16))) T kb1[TILE];
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h2 = lane >> 5, l32 = lane & 31;
+  const int nqt = S / QT;
+  const int BH = gridDim.x / nqt;
+  const int qt = nqt - 1 - (int)(blockIdx.x / BH);  // heavy (late) query tiles first
+  const int bh = blockIdx.x % BH;
+  const int hq = bh % Hq, b = bh / Hq;
+  const int hk = hq / (Hq / Hkv);
+  const int q0 = qt * QT, qw = q0 + wid * 32;
+  const int qrow = qw + l32;
+
+  const T* Kb = K + (long)b * S * ldk + hk * D;
+  const T* dsr = dS + ((long)(b * Hq + hq) * S + qrow) * S + 4 * h2;  // this lane's dS row
+
+  LaneOff<T, D> lo;
+  lo.init(lane);
+  f32x16 dqt[NDB];
+#pragma unroll
+  for (int i = 0; i < NDB; ++i) dqt[i] = f32x16{};
+
+  const int nkt = (q0 + QT) / KT;  // causal: key tiles up to the block's last query
+  const int lastw = (qw + 31) / KT;  // this wave's last (diagonal) tile
+  // B operand of k-step k4 (keys 16 k4 ..): the k order of lo.tr's transposed A fragment, i.e.
+  // keys 16 k4 + {4 h2 .. 4 h2 + 3} then 16 k4 + 8 + {4 h2 .. +3}
+  auto load_ds = [&](int kt, V8<T> (&f)[4]) {
+#pragma unroll
+    for (int k4 = 0; k4 < 4; ++k4) {
+      const uint2 a = *reinterpret_cast<const uint2*>(dsr + kt * KT + 16 * k4);
+      const uint2 c = *reinterpret_cast<const uint2*>(dsr + kt * KT + 16 * k4 + 8);
+      f[k4] = __builtin_bit_cast(V8<T>, make_uint4(a.x, a.y, c.x, c.y));
+    }
+  };
+
+  GStage<T, D, KT, NW> gk;
+  gk.init(ldk);
+  gk.issue(Kb, kb0);
+  V8<T> fc[4], fn[4];
+  if (0 <= lastw) load_ds(0, fc);
+  __syncthreads();
+
+  auto body = [&](auto cc, int kt) {
+    constexpr int CUR = decltype(cc)::value;
+    const T* Kt = CUR ? kb1 : kb0;
+    if (kt + 1 < nkt) gk.issue(Kb + (long)(kt + 1) * KT * ldk, CUR ? kb0 : kb1);
+    if (kt <= lastw) {
+      if (kt + 1 <= lastw) load_ds(kt + 1, fn);
+      if (kt == lastw) {  // diagonal tile: dS of keys past this lane's query was never written
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int key = kt * KT + 16 * k4 + (j < 4 ? 4 * h2 + j : 8 + 4 * h2 + j - 4);
+            if (key > qrow) fc[k4][j] = (T)0.f;
+          }
+      }
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4)
+#pragma unroll
+        for (int db = 0; db < NDB; ++db) dqt[db] = mfma(lo.tr(Kt, 16 * k4, db), fc[k4], dqt[db]);
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) fc[k4] = fn[k4];
+    }
+    __syncthreads();  // the next K tile landed (vmcnt(0)); this buffer is free
+  };
+  for (int kt = 0; kt < nkt; kt += 2) {
+    body(IC<0>{}, kt);
+    if (kt + 1 < nkt) body(IC<1>{}, kt + 1);
+  }
+  store_rows16<T, NDB>(dqt, scale, dQ + ((long)b * S + qrow) * lddq + hq * D, true, h2);
+}
+
 }  // namespace attn
 }  // namespace pra
 
@@ -1250,11 +1351,43 @@ hipError_t attn_fwd_t(const void* q, const void* k, const void* v, void* o, floa
   return hipGetLastError();
 }
 
+// Kernel choices of the backward, shared by the launcher and pra_attn_bwd_ds_bytes.
+// dK/dV: D = 64: 64 KB of LDS and <= 256 VGPRs, so two pipelined one-wave blocks share a CU and hide
+// each other's prologue (B16 S2048 H16: 0.74 -> 0.68 ms bwd). At D = 128 the pipelined kernel wins
+// only while the two-wave kernel's grid ((S/256) Hkv B blocks, one per CU) is at most one round of
+// the chip's 256 CUs, where its causal work imbalance is exposed: S 8192 GQA 32/8 bwd B1
+// 2.56 -> 1.98 ms with p2, but B4 7.30 (two-wave) vs 7.89 ms (p2) (profiles/attn_dkdv_select_r2.log).
+// PRA_DKDV_IMPL: 1 = pipelined, 0 = two-wave, unset = by shape (read per call; tests switch it).
+static bool dkdv_use_p2(int B, int S, int Hq, int Hkv, int D) {
+  const char* impl_s = getenv("PRA_DKDV_IMPL");
+  const int impl_env = impl_s ? atoi(impl_s) : -1;
+  const long grid2 = (long)(S / 256) * Hkv * B;
+  return impl_env == 1 || (impl_env < 0 && (D == 64 || ((long)(Hq / Hkv) * S >= 8192 && grid2 <= 256)));
+}
+static int dkdv_nw_env() {
+  static const int v = [] {
+    const char* e = getenv("PRA_DKDV_NW");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+// dS-materializing path (causal): dK/dV (two-wave, 8 waves) also writes dS, then a one-GEMM dQ
+// kernel reads it -- S and dP are computed once instead of in both kernels. Needs a [B, Hq, S, S]
+// 16-bit workspace (capped at 8 GiB). PRA_ATTN_DS (read per call): 0 = off, 1 = on.
+static size_t ds_path_bytes(int B, int S, int Hq, int Hkv, int D, int causal) {
+  const char* e = getenv("PRA_ATTN_DS");
+  if (!(e ? atoi(e) != 0 : false)) return 0;
+  if (!causal || D != 128 || S % 256 || Hq > PRE_MAXH) return 0;
+  if (dkdv_use_p2(B, S, Hq, Hkv, D) || dkdv_nw_env() == 4) return 0;
+  const size_t bytes = (size_t)B * Hq * S * S * 2;
+  return bytes <= (8ull << 30) ? bytes : 0;
+}
+
 template <typename T>
 hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o, const void* dout,
                         const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int S, int Hq, int Hkv,
                         int D, long ldq, long ldk, long ldv, long ldo, long lddo, long lddq, long lddk, long lddv,
-                        float scale, int causal, int skv, hipStream_t st) {
+                        float scale, int causal, int skv, void* ds_ws, size_t ds_bytes, hipStream_t st) {
   if (S % 128 || (D != 64 && D != 128) || Hq % Hkv) return hipErrorInvalidValue;
   if (ldq % 8 || ldk % 8 || ldv % 8 || ldo % 8 || lddo % 8 || lddq % 8 || lddk % 8 || lddv % 8)
     return hipErrorInvalidValue;
@@ -1263,6 +1396,18 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
     const char* e = getenv("PRA_ATTN_BWD_PRIO");
     return e ? atoi(e) : 0;
   }();
+  if (ds_ws != nullptr && ds_bytes >= ds_path_bytes(B, S, Hq, Hkv, D, causal) &&
+      ds_path_bytes(B, S, Hq, Hkv, D, causal) > 0) {
+    // delta = rowsum(dO * O) first (the dK/dV kernel reads it), then dK/dV + dS, then dQ from dS
+    hipLaunchKernelGGL((bwd_pre_kernel<T, 128>), dim3(B * (S / PRE_QB)), dim3(256), 0, st, (const T*)o,
+                       (const T*)dout, delta, B, S, Hq, ldo, lddo);
+    hipLaunchKernelGGL((bwd_dkdv_kernel<T, 128, true, 8, true>), dim3((S / 256) * Hkv * B), dim3(512), 0, st,
+                       (const T*)q, (const T*)k, (const T*)v, (const T*)dout, lse, (const float*)delta, (T*)dk,
+                       (T*)dv, S, Hq, Hkv, ldq, ldk, ldv, lddo, lddk, lddv, scale, sl2, bwd_prio, skv, (T*)ds_ws);
+    hipLaunchKernelGGL((bwd_dq_ds_kernel<T, 128, 8>), dim3((S / 256) * Hq * B), dim3(512), 0, st, (const T*)k,
+                       (const T*)ds_ws, (T*)dq, S, Hq, Hkv, ldk, lddq, scale);
+    return hipGetLastError();
+  }
   // dQ first: it also computes delta = rowsum(dO * O), which the dK/dV kernel reads
   // (PRA_ATTN_DELTA_PRE=1: a separate preprocess kernel computes it, read per call for A/B tests)
   const char* dpre_s = getenv("PRA_ATTN_DELTA_PRE");
@@ -1306,23 +1451,9 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
 #undef LAUNCH
   }
   {
-    static const int nw_env = [] {
-      const char* e = getenv("PRA_DKDV_NW");
-      return e ? atoi(e) : 0;
-    }();
-    // PRA_DKDV_IMPL: 1 = one-wave-per-SIMD pipelined kernel, 0 = two-wave kernel, unset = by shape:
-    // at D = 128 the pipelined kernel pays a per-block prologue (64 KB of K/V) that only long query
-    // loops amortize (measured: S 8192 GQA 4:1 bwd 2.70 -> 2.03 ms; S 2048 MHA 1.30 -> 1.38 ms)
-    const char* impl_s = getenv("PRA_DKDV_IMPL");  // read per call (tests switch it)
-    const int impl_env = impl_s ? atoi(impl_s) : -1;
+    const int nw_env = dkdv_nw_env();
     const int nw = (nw_env == 4 || S % 256) ? 4 : 8;
-    // D = 64: 64 KB of LDS and <= 256 VGPRs, so two blocks share a CU and hide each other's prologue
-    // (B16 S2048 H16: 0.74 -> 0.68 ms bwd). At D = 128 the pipelined kernel wins only while the
-    // two-wave kernel's grid ((S/256) Hkv B blocks, one per CU) is at most one round of the chip's
-    // 256 CUs, where its causal work imbalance is exposed: S 8192 GQA 32/8 bwd B1 2.56 -> 1.98 ms
-    // with p2, but B4 7.30 (two-wave) vs 7.89 ms (p2) (profiles/attn_dkdv_select_r2.log).
-    const long grid2 = (long)(S / 256) * Hkv * B;
-    const bool p2 = impl_env == 1 || (impl_env < 0 && (D == 64 || ((long)(Hq / Hkv) * S >= 8192 && grid2 <= 256)));
+    const bool p2 = dkdv_use_p2(B, S, Hq, Hkv, D);
     if (p2 && nw_env == 0) {
       dim3 g1((S / 128) * Hkv * B);
 #define LAUNCH1(DD, CC)                                                                                       \
@@ -1369,15 +1500,21 @@ hipError_t pra_attn_fwd(int dtype, const void* q, const void* k, const void* v, 
 hipError_t pra_attn_bwd(int dtype, const void* q, const void* k, const void* v, const void* o, const void* dout,
                         const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int S, int Hq, int Hkv,
                         int D, long ldq, long ldk, long ldv, long ldo, long lddo, long lddq, long lddk, long lddv,
-                        float scale, int causal, int skv, hipStream_t st) {
+                        float scale, int causal, int skv, void* ds_ws, size_t ds_bytes, hipStream_t st) {
   if (skv <= 0 || skv > S) return hipErrorInvalidValue;
   if (dtype == pra::kBF16)
     return attn_bwd_t<__bf16>(q, k, v, o, dout, lse, delta, dq, dk, dv, B, S, Hq, Hkv, D, ldq, ldk, ldv, ldo, lddo,
-                              lddq, lddk, lddv, scale, causal, skv, st);
+                              lddq, lddk, lddv, scale, causal, skv, ds_ws, ds_bytes, st);
   if (dtype == pra::kF16)
     return attn_bwd_t<_Float16>(q, k, v, o, dout, lse, delta, dq, dk, dv, B, S, Hq, Hkv, D, ldq, ldk, ldv, ldo, lddo,
-                                lddq, lddk, lddv, scale, causal, skv, st);
+                                lddq, lddk, lddv, scale, causal, skv, ds_ws, ds_bytes, st);
   return hipErrorInvalidValue;
+}
+
+// Workspace bytes the backward would use for the dS-materializing path (0: the path is off for
+// this shape / setting; the caller then passes no workspace).
+size_t pra_attn_bwd_ds_bytes(int B, int S, int Hq, int Hkv, int D, int causal) {
+  return ds_path_bytes(B, S, Hq, Hkv, D, causal);
 }
 
 }  // extern "C"

@@ -61,5 +61,6 @@ hipError_t pra_attn_fwd(int dtype, const void* q, const void* k, const void* v, 
 hipError_t pra_attn_bwd(int dtype, const void* q, const void* k, const void* v, const void* o, const void* dout,
                         const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int S, int Hq, int Hkv,
                         int D, long ldq, long ldk, long ldv, long ldo, long lddo, long lddq, long lddk, long lddv,
-                        float scale, int causal, int skv, hipStream_t st);
+                        float scale, int causal, int skv, void* ds_ws, size_t ds_bytes, hipStream_t st);
+size_t pra_attn_bwd_ds_bytes(int B, int S, int Hq, int Hkv, int D, int causal);
 }

@@ -280,6 +280,34 @@ def test_attention_bwd_dkdv_kernels(cuda, monkeypatch, impl, B, S, Hq, Hkv, D, c
     assert torch.equal(dq, dq2) and torch.equal(dk, dk2) and torch.equal(dv, dv2)
 
 
+@pytest.mark.parametrize("B,S,Hq,Hkv", [(1, 1024, 4, 1), (2, 512, 4, 4), (1, 2048, 2, 2)])
+def test_attention_bwd_materialized_ds(cuda, monkeypatch, B, S, Hq, Hkv):
+    """dS-materializing backward (PRA_ATTN_DS=1: dK/dV also writes dS, dQ is one GEMM over it) vs
+    the fp32 oracle; dK/dV bit-identical to the default path, dQ deterministic."""
+    monkeypatch.setenv("PRA_DKDV_IMPL", "0")
+    monkeypatch.setenv("PRA_ATTN_DELTA_PRE", "1")  # same delta = rowsum(dO*O) kernel as the dS path
+    C = _ext.native()
+    _, q, k, v = _qkv(cuda, B, S, Hq, Hkv, 128, seed=11)
+    scale = 1 / math.sqrt(128)
+    o, lse = C.attn_fwd(q, k, v, scale, True)
+    do = torch.randn(B, S, Hq, 128, device=cuda).bfloat16()
+    outs = {}
+    for ds in ("0", "1", "1"):
+        monkeypatch.setenv("PRA_ATTN_DS", ds)
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        C.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, True)
+        if ds in outs:
+            assert all(torch.equal(a, b) for a, b in zip(outs[ds], (dq, dk, dv)))  # deterministic
+        outs[ds] = (dq, dk, dv)
+    qf, kf, vf = (t.float().requires_grad_() for t in (q, k, v))
+    of, _ = R.attention_lse_ref(qf, kf, vf, True, scale)
+    of.backward(do.float())
+    for got, want in zip(outs["1"], (qf.grad, kf.grad, vf.grad)):
+        assert _rel(got, want) < 3e-2, (_rel(got, want))
+    assert torch.equal(outs["1"][1], outs["0"][1]) and torch.equal(outs["1"][2], outs["0"][2])
+    assert _rel(outs["1"][0], outs["0"][0].float()) < 1e-2
+
+
 def test_single_hip_runtime_loaded(cuda):
     """The extension must bind to torch's HIP runtime, not load a second copy."""
     maps = open("/proc/self/maps").read()
