@@ -469,6 +469,28 @@ at::Tensor transpose2d(const at::Tensor& src, c10::optional<at::Tensor> out) {
   return dst;
 }
 
+// out [M, N] (+)= a^T b with a [K, M], b [K, N] (both row-major, K = tokens): the weight gradient
+// dW = dY^T X straight from the activations (no transposed copies), hand-written MFMA kernel.
+void wgrad_mm_(const at::Tensor& a, const at::Tensor& b, at::Tensor out, bool accumulate) {
+  const Range range_("pyrecover::wgrad_mm");
+  check_dev(a, "a");
+  check_row_major(a, "a");
+  check_row_major(b, "b");
+  check_row_major(out, "out");
+  same_dev(a, b, "b");
+  same_dev(a, out, "out");
+  const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
+  TORCH_CHECK(b.size(0) == K && out.size(0) == M && out.size(1) == N, "wgrad_mm: shapes [K,M] x [K,N] -> [M,N]");
+  TORCH_CHECK(a.scalar_type() == b.scalar_type() && a.scalar_type() == out.scalar_type() && a.element_size() == 2,
+              "wgrad_mm: bf16/fp16 operands of one dtype");
+  TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 32 == 0 && K > 0, "wgrad_mm: M, N % 256 and K % 32");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && out.stride(0) % 8 == 0, "wgrad_mm: 16-B rows");
+  const c10::DeviceGuard guard(a.device());
+  check(pra_wgrad_gemm(dt(a), a.data_ptr(), b.data_ptr(), out.data_ptr(), (int)M, (int)N, (int)K, a.stride(0),
+                       b.stride(0), out.stride(0), accumulate ? 1 : 0, stream_of(a)),
+        "wgrad_mm");
+}
+
 // returns fp32 [2] = {norm, clip_coef}
 at::Tensor grad_norm(const at::Tensor& x, double max_norm, double pre_scale) {
   const Range range_("pyrecover::grad_norm");
@@ -631,6 +653,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("bc1"), py::arg("bc2_sqrt"),
         py::arg("gscale"), py::arg("gscale_dev") = py::none(), py::arg("hyper_dev") = py::none());
   m.def("grad_norm", &grad_norm);
+  m.def("wgrad_mm_", &wgrad_mm_);
   m.def("transpose2d", &transpose2d, py::arg("src"), py::arg("out") = py::none());
   m.def("swiglu_bwd_t_", &swiglu_bwd_t_);
   m.def("swiglu_fwd_t", &swiglu_fwd_t);

@@ -251,6 +251,21 @@ __device__ __forceinline__ void put8(uint16_t* row, const float* v) {
   *reinterpret_cast<uint4*>(row) = *reinterpret_cast<const uint4*>(tmp);
 }
 
+template <typename T>
+__device__ __forceinline__ void unpack8(const uint4& w, float (&o)[8]) {
+  const T* e = reinterpret_cast<const T*>(&w);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = to_f<T>(e[j]);
+}
+
+template <typename T>
+__device__ __forceinline__ uint4 pack8(const float (&v)[8]) {
+  T tmp[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) tmp[j] = from_f<T>(v[j]);
+  return *reinterpret_cast<const uint4*>(tmp);
+}
+
 // swiglu_fwd_t: a = silu(g) * u (row-major, for the W2 forward GEMM) and aT = a^T (K-contiguous
 // operand of the W2 weight-gradient GEMM, kept for the backward instead of a).
 template <typename T>
@@ -309,6 +324,62 @@ __global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(const T* __restrict__
   store_tile_t(tu, reinterpret_cast<uint16_t*>(guT), ntok, F + c0, t0);
 }
 
+// Same op, loads hoisted: gu is updated in place, so it cannot be __restrict__, and in the kernel
+// above the compiler may not move iteration 1's loads of gu above iteration 0's stores to it -- each
+// lane has only one row's three 16-B loads in flight at a time. Here every load of the block's
+// NT 64x64 tiles is issued before the first store (NT = 2: 6 x 16 B x 2 in flight per lane, each
+// row 256 contiguous bytes per operand).
+template <typename T, int NT>
+__global__ __launch_bounds__(256) void swiglu_bwd_t_hoist_kernel(const T* __restrict__ dy, T* gu,
+                                                                 T* __restrict__ guT, int F, int ldgu, int lddy,
+                                                                 long ntok) {
+  __shared__ __attribute__((aligned(16))) uint16_t tg[NT][64][72], tu[NT][64][72];
+  constexpr int CPR = 8 * NT;  // 16-B chunks per tile row
+  constexpr int IT = 2 * NT;   // rows x chunks per lane
+  const long t0 = (long)blockIdx.y * 64;
+  const int c0 = blockIdx.x * 64 * NT;
+  uint4 G[IT], U[IT], DY[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int idx = threadIdx.x + 256 * i, r = idx / CPR, cc = idx % CPR;
+    const long t = t0 + r;
+    const int col = c0 + cc * 8;
+    G[i] = *reinterpret_cast<const uint4*>(gu + t * ldgu + col);
+    U[i] = *reinterpret_cast<const uint4*>(gu + t * ldgu + F + col);
+    DY[i] = *reinterpret_cast<const uint4*>(dy + t * lddy + col);
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int idx = threadIdx.x + 256 * i, r = idx / CPR, cc = idx % CPR;
+    const long t = t0 + r;
+    const int col = c0 + cc * 8;
+    float gv[8], uv[8], dv[8], og[8], ou[8];
+    unpack8<T>(G[i], gv);
+    unpack8<T>(U[i], uv);
+    unpack8<T>(DY[i], dv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {  // identical math / rounding to swiglu_bwd_kernel
+      const float sg = 1.f / (1.f + __expf(-gv[j]));
+      const float a = rnd<T>(gv[j] * sg);
+      const float da = rnd<T>(dv[j] * uv[j]);
+      ou[j] = dv[j] * a;
+      og[j] = da * sg * (1.f + gv[j] * (1.f - sg));
+    }
+    const uint4 pg = pack8<T>(og), pu = pack8<T>(ou);
+    *reinterpret_cast<uint4*>(gu + t * ldgu + col) = pg;
+    *reinterpret_cast<uint4*>(gu + t * ldgu + F + col) = pu;
+    const int tl = cc / 8, ch = cc % 8;
+    *reinterpret_cast<uint4*>(&tg[tl][r][swz(r, ch) * 8]) = pg;
+    *reinterpret_cast<uint4*>(&tu[tl][r][swz(r, ch) * 8]) = pu;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int tl = 0; tl < NT; ++tl) {
+    store_tile_t(tg[tl], reinterpret_cast<uint16_t*>(guT), ntok, c0 + 64 * tl, t0);
+    store_tile_t(tu[tl], reinterpret_cast<uint16_t*>(guT), ntok, F + c0 + 64 * tl, t0);
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void rope_t_kernel(T* x, T* __restrict__ xT, const float2* __restrict__ tab,
                                                      int ld, int nrot, int D, int S, float sign, long ntok) {
@@ -350,21 +421,6 @@ __global__ __launch_bounds__(256) void rope_t_kernel(T* x, T* __restrict__ xT, c
 // 64-column tile, lane (g, ch) owns tokens 8g..8g+7 x columns 8ch..8ch+7, so its eight row
 // vectors are the 8x8 block the transposed store needs (transpose8x8_b16). No LDS, no barrier,
 // every operand's eight row loads issued before any math. Same math and rounding as above.
-template <typename T>
-__device__ __forceinline__ void unpack8(const uint4& w, float (&o)[8]) {
-  const T* e = reinterpret_cast<const T*>(&w);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = to_f<T>(e[j]);
-}
-
-template <typename T>
-__device__ __forceinline__ uint4 pack8(const float (&v)[8]) {
-  T tmp[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) tmp[j] = from_f<T>(v[j]);
-  return *reinterpret_cast<const uint4*>(tmp);
-}
-
 // tile of this wave (tiles_c column tiles per 64-token row of tiles); false past the end
 __device__ __forceinline__ bool wave_tile(int tiles_c, long n_tiles, long& t0, int& c0, int& g, int& ch) {
   const long tile = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -502,6 +558,12 @@ static int pra_transpose_mode() {  // 0 default, 1 lds, 2 reg
 }
 static bool pra_use_lds_transpose() { return pra_transpose_mode() == 1; }
 static bool pra_use_lds_swiglu_bwd_t() { return pra_transpose_mode() != 2; }
+// LDS swiglu_bwd_t generation: 0 = one row in flight per lane, 1 = hoisted loads (64x64 tile),
+// 2 = hoisted loads over two 64x64 tiles (default). Read per call (A/B in one process).
+static int pra_swiglu_bwd_hoist() {
+  const char* e = getenv("PRA_SWIGLU_BWD");
+  return e ? atoi(e) : 2;
+}
 
 extern "C" {
 
@@ -601,7 +663,21 @@ hipError_t pra_swiglu_bwd_t(int dtype, const void* dy, void* gu, void* guT, long
                                           n_tiles));
     return hipGetLastError();
   }
+  const int hoist = pra_swiglu_bwd_hoist();
+  if (hoist == 2 && F % 128 == 0) {
+    dim3 grid((unsigned)(F / 128), (unsigned)(ntok / 64));
+    PRA_DISPATCH_16BIT(dtype, T,
+                       hipLaunchKernelGGL((pra::swiglu_bwd_t_hoist_kernel<T, 2>), grid, dim3(256), 0, s, (const T*)dy,
+                                          (T*)gu, (T*)guT, F, ldgu, lddy, ntok));
+    return hipGetLastError();
+  }
   dim3 grid((unsigned)(F / 64), (unsigned)(ntok / 64));
+  if (hoist) {
+    PRA_DISPATCH_16BIT(dtype, T,
+                       hipLaunchKernelGGL((pra::swiglu_bwd_t_hoist_kernel<T, 1>), grid, dim3(256), 0, s, (const T*)dy,
+                                          (T*)gu, (T*)guT, F, ldgu, lddy, ntok));
+    return hipGetLastError();
+  }
   PRA_DISPATCH_16BIT(dtype, T,
                      hipLaunchKernelGGL((pra::swiglu_bwd_t_kernel<T>), grid, dim3(256), 0, s, (const T*)dy, (T*)gu,
                                         (T*)guT, F, ldgu, lddy, ntok));

@@ -101,9 +101,42 @@ def _tn_ok(t):
             and t.size(1) % 64 == 0 and t.stride(0) % 8 == 0)
 
 
+# Weight gradients on the hand-written MFMA GEMM (csrc/kernels/gemm_wgrad.hip, default): dW = dY^T X
+# read straight from the row-major activations, transposed inside the LDS read
+# (ds_read_b64_tr_b16), so neither the TN transposes nor the transposing epilogues (a^T, dgu^T,
+# dqkv^T) are needed. PYRECOVER_WGRAD=lib restores hipBLASLt on transposed operands.
+WGRAD_HIP = os.environ.get("PYRECOVER_WGRAD", "hip") == "hip"
+
+
+def _hip_wgrad_dims(t, tokens, *cols) -> bool:
+    """The MFMA weight-gradient kernel's shape rules: K = tokens % 32, every output dim % 256."""
+    return (WGRAD_HIP and _ext.hip16(t) and tokens % 32 == 0 and tokens > 0
+            and all(c % 256 == 0 for c in cols))
+
+
+def _hip_wgrad_ok(dy2, x2) -> bool:
+    return (dy2.dim() == 2 and x2.dim() == 2 and dy2.dtype == x2.dtype and dy2.device == x2.device
+            and dy2.size(0) == x2.size(0) and _hip_wgrad_dims(dy2, dy2.size(0), dy2.size(1), x2.size(1))
+            and all(t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0 for t in (dy2, x2)))
+
+
+def _hip_wgrad(slot, dy2, x2, shape):
+    """slot (+)= dy2^T x2 on the MFMA kernel (beta = 1 when the slot already holds a gradient)."""
+    if hasattr(slot, "take"):  # flat GradSlot: write into the flat gradient buffer in place
+        acc = slot.take()
+        _ext.require_for(dy2).wgrad_mm_(dy2, x2, slot.view.view(shape), acc)
+        slot.done()
+    else:
+        buf, acc = slot.begin(dy2)
+        _ext.require_for(dy2).wgrad_mm_(dy2, x2, buf.view(shape), acc)
+        slot.end(buf)
+
+
 def _wgrad_into(slot, dy2, x2, shape):
     """slot <- dy2^T x2 (dy2 [T, out], x2 [T, in])."""
-    if TN_WGRAD and _tn_ok(dy2) and _tn_ok(x2):
+    if _hip_wgrad_ok(dy2, x2):
+        _hip_wgrad(slot, dy2, x2, shape)
+    elif TN_WGRAD and _tn_ok(dy2) and _tn_ok(x2):
         C = _ext.require_for(dy2)
         slot.mm_(C.transpose2d(dy2), C.transpose2d(x2).t(), shape)
     else:
@@ -331,7 +364,8 @@ class _AttentionBlock(torch.autograd.Function):
         dk = dqkv[:, nq:nq + nk].view(B, S, Hkv, D)
         dv = dqkv[:, nq + nk:].view(B, S, Hkv, D)
         _attn_bwd(q, k, v, o, do, lse, dq, dk, dv, ctx.scale, causal)
-        if TN_WGRAD and _tn_ok(dqkv) and _tn_ok(x2) and T % S == 0 and D % 8 == 0:
+        if (not _hip_wgrad_ok(dqkv, x2) and TN_WGRAD and _tn_ok(dqkv) and _tn_ok(x2) and T % S == 0
+                and D % 8 == 0):
             # inverse RoPE in place + dqkv^T in one pass, for the K-contiguous weight-grad GEMM
             C = _ext.require_for(dqkv)
             dqkvT = C.rope_t_(dqkv, nq + nk, tab, D, S, True)
@@ -382,7 +416,9 @@ class _SwiGLUMLP(torch.autograd.Function):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
         gu = torch.mm(x2, w13.t())
-        if TN_WGRAD and _tn_ok(gu) and (gu.shape[1] // 2) % 64 == 0:
+        F = gu.shape[1] // 2
+        if (not _hip_wgrad_dims(gu, gu.shape[0], shape[-1], F) and TN_WGRAD and _tn_ok(gu)
+                and F % 64 == 0):
             # a^T (K-contiguous operand of the W2 weight gradient) is written in the same pass and
             # kept instead of a
             a, a_saved = _ext.require_for(gu).swiglu_fwd_t(gu)
@@ -407,8 +443,12 @@ class _SwiGLUMLP(torch.autograd.Function):
             dyT = _ext.require_for(dy2).transpose2d(dy2) if _tn_ok(dy2) else dy2.t()
             slot2.mm_(dyT, a.t(), tuple(w2.shape))
         else:
-            slot2.mm_(dy2.t(), a, tuple(w2.shape))
-        if TN_WGRAD and _tn_ok(gu) and _tn_ok(x2) and _tn_ok(da):
+            _wgrad_into(slot2, dy2, a, tuple(w2.shape))
+        if _hip_wgrad_ok(gu, x2):
+            dgu = _swiglu_bwd_(da, gu)  # in place over gu; no transposed copy for the MFMA wgrad
+            dx = torch.mm(dgu, w13_t.t()) if w13_t is not None else torch.mm(dgu, w13)
+            _hip_wgrad(slot13, dgu, x2, tuple(w13.shape))
+        elif TN_WGRAD and _tn_ok(gu) and _tn_ok(x2) and _tn_ok(da):
             # SwiGLU backward in place over gu, writing dgu^T in the same pass
             C = _ext.require_for(gu)
             dguT = C.swiglu_bwd_t_(da, gu)

@@ -324,11 +324,16 @@ def test_transpose2d_exact(cuda, R, C):
     assert torch.equal(C_.transpose2d(xs), xs.t().contiguous())
 
 
-@pytest.mark.parametrize("T,F", [(256, 192), (64, 192), (2048, 1024)])
-def test_swiglu_bwd_t_matches_swiglu_bwd_exactly(cuda, T, F):
+@pytest.mark.parametrize("gen", ["0", "1", "2"])
+@pytest.mark.parametrize("T,F,dtype", [(256, 192, torch.bfloat16), (64, 192, torch.bfloat16),
+                                       (2048, 1024, torch.bfloat16), (128, 256, torch.float16)])
+def test_swiglu_bwd_t_matches_swiglu_bwd_exactly(cuda, T, F, dtype, gen, monkeypatch):
+    # every LDS generation (PRA_SWIGLU_BWD, read per call; F = 192 makes generation 2 fall back to
+    # the one-tile kernel) against the row-major kernel
+    monkeypatch.setenv("PRA_SWIGLU_BWD", gen)
     C_ = _ext.native()
-    gu = torch.randn(T, 2 * F, device=cuda).bfloat16()
-    dy = torch.randn(T, F, device=cuda).bfloat16()
+    gu = torch.randn(T, 2 * F, device=cuda).to(dtype)
+    dy = torch.randn(T, F, device=cuda).to(dtype)
     ref = C_.swiglu_bwd(dy, gu.clone(), None)
     g2 = gu.clone()
     guT = C_.swiglu_bwd_t_(dy, g2)
@@ -406,3 +411,52 @@ def test_adamw_t_matches_flat_adamw_plus_transpose(cuda, monkeypatch, strip, row
     for x, y in zip(a, b):
         assert torch.equal(x, y)
     assert torch.equal(pt, pt_ref)
+
+
+# ---------------------------------------------------------------------------------------
+# Weight-gradient MFMA GEMM (csrc/kernels/gemm_wgrad.hip): out (+)= a^T b on row-major operands
+@pytest.mark.parametrize("mfma", ["16", "32"])
+@pytest.mark.parametrize("K,M,N,dtype", [(32, 256, 256, torch.bfloat16), (2048, 768, 512, torch.bfloat16),
+                                         (4096, 512, 1024, torch.float16), (96, 1280, 256, torch.bfloat16)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_wgrad_mm_vs_fp32(cuda, monkeypatch, mfma, K, M, N, dtype, accumulate):
+    monkeypatch.setenv("PRA_WGRAD_MFMA", mfma)
+    C_ = _ext.native()
+    g = torch.Generator(device=cuda)
+    g.manual_seed(K + M + N)
+    a = torch.randn(K, M, device=cuda, generator=g).to(dtype)
+    b = torch.randn(K, N, device=cuda, generator=g).to(dtype)
+    c0 = torch.randn(M, N, device=cuda, generator=g).to(dtype)
+    out = c0.clone()
+    C_.wgrad_mm_(a, b, out, accumulate)
+    ref = a.double().t() @ b.double() + (c0.double() if accumulate else 0)
+    # one rounding of the fp32 result to the 16-bit output
+    err = ((out.double() - ref).abs() / (ref.abs() + math.sqrt(K))).max().item()
+    assert err < (1e-2 if dtype == torch.bfloat16 else 2e-3), err
+    out2 = c0.clone()
+    C_.wgrad_mm_(a, b, out2, accumulate)
+    assert torch.equal(out, out2)  # deterministic
+
+
+def test_wgrad_mm_strided_rows_and_slot_views(cuda):
+    """Operands that are column slices of wider activations (row stride > width) and an output
+    that is a view into a larger flat buffer, as the flat gradient slots are."""
+    C_ = _ext.native()
+    torch.manual_seed(3)
+    big_a = torch.randn(512, 1024 + 256, device=cuda).bfloat16()
+    big_b = torch.randn(512, 512 + 64, device=cuda).bfloat16()
+    a, b = big_a[:, 256:], big_b[:, 64:]
+    flat = torch.zeros(1024 * 512 + 4096, device=cuda, dtype=torch.bfloat16)
+    out = flat[4096:].view(1024, 512)
+    C_.wgrad_mm_(a, b, out, False)
+    ref = a.float().t() @ b.float()
+    assert ((out.float() - ref).norm() / ref.norm()).item() < 5e-3
+    assert flat[:4096].abs().sum().item() == 0
+
+
+def test_wgrad_mm_rejects_bad_shapes(cuda):
+    C_ = _ext.native()
+    a = torch.randn(64, 300, device=cuda).bfloat16()
+    b = torch.randn(64, 256, device=cuda).bfloat16()
+    with pytest.raises(RuntimeError):
+        C_.wgrad_mm_(a, b, torch.empty(300, 256, device=cuda, dtype=torch.bfloat16), False)
