@@ -486,8 +486,20 @@ void wgrad_mm_(const at::Tensor& a, const at::Tensor& b, at::Tensor out, bool ac
   TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 32 == 0 && K > 0, "wgrad_mm: M, N % 256 and K % 32");
   TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && out.stride(0) % 8 == 0, "wgrad_mm: 16-B rows");
   const c10::DeviceGuard guard(a.device());
+  // scratch of the split tail (fp32 partial tiles + tickets), from the caching allocator so it is
+  // graph-capture safe; only when the tiles do not fill whole rounds of the CUs
+  const int64_t nwg = (M / 256) * (N / 256);
+  int cus = 0;
+  TORCH_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, a.device().index()) == hipSuccess,
+              "wgrad_mm: device attribute");
+  at::Tensor ws, tickets;
+  if (nwg > cus && nwg % cus != 0) {
+    ws = at::empty({(int64_t)pra_wgrad_ws_floats()}, a.options().dtype(at::kFloat));
+    tickets = at::empty({(int64_t)pra_wgrad_ticket_count()}, a.options().dtype(at::kInt));
+  }
   check(pra_wgrad_gemm(dt(a), a.data_ptr(), b.data_ptr(), out.data_ptr(), (int)M, (int)N, (int)K, a.stride(0),
-                       b.stride(0), out.stride(0), accumulate ? 1 : 0, stream_of(a)),
+                       b.stride(0), out.stride(0), accumulate ? 1 : 0, ws.defined() ? ws.data_ptr<float>() : nullptr,
+                       tickets.defined() ? tickets.data_ptr<int>() : nullptr, stream_of(a)),
         "wgrad_mm");
 }
 

@@ -271,23 +271,32 @@ __device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
+// Work decomposition: tiles of 256 x 256 in group-M order (8 M-tiles per group). When the tile
+// count is not a multiple of the CU count, the R tiles of the partial last round are split S ways
+// over K (the launcher picks S so the split units fill whole rounds best): grid = (nwg - R) whole
+// tiles + R * S split units, dispatched in that order. Each split unit writes its fp32 partial to
+// ws and takes a ticket; the last arriver of a tile sums the S partials in part order (its own from
+// ws too) -- deterministic, and nothing ever waits on another
+// workgroup.
 template <typename T, bool ACC>
 __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, const T* __restrict__ B,
                                                       T* __restrict__ C, int M, int N, int K, long lda, long ldb,
-                                                      long ldc) {
+                                                      long ldc, float* __restrict__ ws, int* __restrict__ tickets,
+                                                      int n_split, int S) {
   __shared__ __attribute__((aligned(1024))) T smem[NS * 2 * TILE];
-  const int tiles_m = M / BM, tiles_n = N / BN, nwg = tiles_m * tiles_n;
-  int wgid;
-  {
-    const int orig = blockIdx.x, xcd = orig % 8, q = nwg / 8, r = nwg % 8;
-    wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
-  }
+  const int tiles_m = M / BM, tiles_n = N / BN, nwg = tiles_m * tiles_n, nk = K / BK;
+  // XCD-contiguous index of workgroup `orig` among n (undo the round-robin placement over the 8 XCDs)
+  auto xcd_remap = [](int orig, int n) {
+    const int xcd = orig % 8, q = n / 8, r = n % 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+  };
   constexpr int GM = 8;
-  const int group = wgid / (GM * tiles_n), first_m = group * GM;
-  const int gsz = min(tiles_m - first_m, GM);
-  const int tm = first_m + (wgid % (GM * tiles_n)) % gsz;
-  const int tn = (wgid % (GM * tiles_n)) / gsz;
-  const long m0 = (long)tm * BM, n0 = (long)tn * BN;
+  auto tile_origin = [&](int lin, long& m0, long& n0) __attribute__((always_inline)) {
+    const int group = lin / (GM * tiles_n), first_m = group * GM;
+    const int gsz = min(tiles_m - first_m, GM);
+    m0 = (long)(first_m + (lin % (GM * tiles_n)) % gsz) * BM;
+    n0 = (long)((lin % (GM * tiles_n)) / gsz) * BN;
+  };
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -300,15 +309,7 @@ __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, c
     offa[i] = r * (int)lda + ch * 8;
     offb[i] = r * (int)ldb + ch * 8;
   }
-  const T* Ab = A + m0;
-  const T* Bb = B + n0;
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) T*)smem;
-  auto dma = [&](int s, int kt, int u) {  // DMA instruction u (0..2NI-1) of stage kt into slot s
-    const int i = u >> 1;
-    const uint32_t base = lds0 + (uint32_t)(s * 2 * TILE + (u & 1) * TILE) * sizeof(T);
-    const T* g = (u & 1) ? Bb + (long)kt * BK * ldb + offb[i] : Ab + (long)kt * BK * lda + offa[i];
-    dma16(g, __builtin_amdgcn_readfirstlane(base + (i * 4 + wid) * 1024));
-  };
 
   // lane offsets of the transposed reads: [column-block parity][lo/hi]
   int oa[2][2], ob[2][2];
@@ -327,97 +328,168 @@ __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, c
     }
   }
   // 16-column block f (0..7) of the wave's 128 columns
-  auto fragA = [&](const T* tile, int f) -> V8<T> {
+  auto fragA = [&](const T* tile, int f) __attribute__((always_inline)) -> V8<T> {
     const i16x4 lo = tr4(tile, oa[f & 1][0] + 512 * (f >> 1));
     const i16x4 hi = tr4(tile, oa[f & 1][1] + 512 * (f >> 1));
     return __builtin_bit_cast(V8<T>, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
   };
-  auto fragB = [&](const T* tile, int f) -> V8<T> {
+  auto fragB = [&](const T* tile, int f) __attribute__((always_inline)) -> V8<T> {
     const i16x4 lo = tr4(tile, ob[f & 1][0] + 512 * (f >> 1));
     const i16x4 hi = tr4(tile, ob[f & 1][1] + 512 * (f >> 1));
     return __builtin_bit_cast(V8<T>, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
   };
 
   f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = K / BK;
-#pragma unroll
-  for (int p = 0; p < NS - 1; ++p)
-#pragma unroll
-    for (int u = 0; u < 2 * NI; ++u) dma(p, min(p, nk - 1), u);
-  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
   V8<T> fa0[8], fb0[8], fa1[8], fb1[8];
-#pragma unroll
-  for (int f = 0; f < 8; ++f) {
-    fa0[f] = fragA(smem, f);
-    fb0[f] = fragB(smem + TILE, f);
-  }
 
-  // step kt (slot s, fragments in ca/cb): m-blocks 0..3 (32 MFMAs); counted wait + barrier publish
-  // stage kt + 1 and free slot (kt - 1) % 4; m-blocks 4..7 in 8 groups of 4 MFMAs, each with 4
-  // fragment reads of stage kt + 1 and one DMA instruction of stage kt + 3.
-  auto step = [&](auto s_c, V8<T> (&ca)[8], V8<T> (&cb)[8], V8<T> (&na)[8], V8<T> (&nb)[8], int kt) {
-    constexpr int s = decltype(s_c)::value, sn = (s + 1) % NS, sd = (s + NS - 1) % NS;
-    const T* nta = smem + sn * 2 * TILE;
+  // acc = sum over the 32-deep stages [k0, k1) of tile (m0, n0)
+  auto run = [&](long m0, long n0, int k0, int k1) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = mfma16(cb[j], ca[i], acc[i][j]);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const T* Ab = A + m0;
+    const T* Bb = B + n0;
+    auto dma = [&](int s, int kt, int u) __attribute__((always_inline)) {  // DMA instruction u (0..2NI-1) of stage kt into slot s
+      const int i = u >> 1;
+      const uint32_t base = lds0 + (uint32_t)(s * 2 * TILE + (u & 1) * TILE) * sizeof(T);
+      const T* g = (u & 1) ? Bb + (long)kt * BK * ldb + offb[i] : Ab + (long)kt * BK * lda + offa[i];
+      dma16(g, __builtin_amdgcn_readfirstlane(base + (i * 4 + wid) * 1024));
+    };
+    // every step issues exactly one stage of DMA (a stage past k1 re-loads stage k1 - 1 into the
+    // slot nobody reads again), so the counted waits are the same on every step
+#pragma unroll
+    for (int p = 0; p < NS - 1; ++p)
+#pragma unroll
+      for (int u = 0; u < 2 * NI; ++u) dma(p, min(k0 + p, k1 - 1), u);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    const int kd = min(kt + NS - 1, nk - 1);
 #pragma unroll
-    for (int gi = 0; gi < 8; ++gi) {
-      // reads: group gi loads fragment gi of A (2 reads) and of B (2 reads)
-      na[gi] = fragA(nta, gi);
-      nb[gi] = fragB(nta + TILE, gi);
-      const int i = 4 + (gi >> 1);
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const int j = 4 * (gi & 1) + jj;
-        acc[i][j] = mfma16(cb[j], ca[i], acc[i][j]);
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-      dma(sd, kd, gi);
+    for (int f = 0; f < 8; ++f) {
+      fa0[f] = fragA(smem, f);
+      fb0[f] = fragB(smem + TILE, f);
     }
+    // step kt (slot s, fragments in ca/cb): m-blocks 0..3 (32 MFMAs); counted wait + barrier
+    // publish stage kt + 1 and free the slot of stage kt - 1; m-blocks 4..7 in 8 groups of 4
+    // MFMAs, each with 4 fragment reads of stage kt + 1 and one DMA instruction of stage kt + 3.
+    auto step = [&](auto s_c, V8<T> (&ca)[8], V8<T> (&cb)[8], V8<T> (&na)[8], V8<T> (&nb)[8], int kt) {
+      constexpr int s = decltype(s_c)::value, sn = (s + 1) % NS, sd = (s + NS - 1) % NS;
+      const T* nta = smem + sn * 2 * TILE;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = mfma16(cb[j], ca[i], acc[i][j]);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const int kd = min(kt + NS - 1, k1 - 1);
+#pragma unroll
+      for (int gi = 0; gi < 8; ++gi) {
+        na[gi] = fragA(nta, gi);
+        nb[gi] = fragB(nta + TILE, gi);
+        const int i = 4 + (gi >> 1);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int j = 4 * (gi & 1) + jj;
+          acc[i][j] = mfma16(cb[j], ca[i], acc[i][j]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        dma(sd, kd, gi);
+      }
+    };
+    for (int kt = k0; kt < k1; kt += NS) {
+      step(IC<0>{}, fa0, fb0, fa1, fb1, kt);
+      if (kt + 1 < k1) step(IC<1>{}, fa1, fb1, fa0, fb0, kt + 1);
+      if (kt + 2 < k1) step(IC<2>{}, fa0, fb0, fa1, fb1, kt + 2);
+      if (kt + 3 < k1) step(IC<3>{}, fa1, fb1, fa0, fb0, kt + 3);
+    }
+    // no LDS-DMA may land after this point (next tile's prologue / end of the workgroup), and no
+    // wave may still read a slot the next prologue overwrites
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   };
-  for (int kt = 0; kt < nk; kt += NS) {
-    step(IC<0>{}, fa0, fb0, fa1, fb1, kt);
-    if (kt + 1 < nk) step(IC<1>{}, fa1, fb1, fa0, fb0, kt + 1);
-    if (kt + 2 < nk) step(IC<2>{}, fa0, fb0, fa1, fb1, kt + 2);
-    if (kt + 3 < nk) step(IC<3>{}, fa1, fb1, fa0, fb0, kt + 3);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup ends
 
   // epilogue: D[n][m] per 16 x 16 block: lane holds m = l & 15, n = 4 (l >> 4) + 0..3 (8 B)
   const int l16 = lane & 15, g4 = lane >> 4;
+  auto store_c = [&](long m0, long n0) __attribute__((always_inline)) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    T* rowp = C + (m0 + 128 * wm + 16 * i + l16) * ldc + n0 + 128 * wn + 4 * g4;
+    for (int i = 0; i < 8; ++i) {
+      T* rowp = C + (m0 + 128 * wm + 16 * i + l16) * ldc + n0 + 128 * wn + 4 * g4;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      T* p = rowp + 16 * j;
-      if constexpr (ACC) {
-        const uint2 old = *reinterpret_cast<const uint2*>(p);
-        const T* o = reinterpret_cast<const T*>(&old);
+      for (int j = 0; j < 8; ++j) {
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        T* p = rowp + 16 * j;
+        if constexpr (ACC) {
+          const uint2 old = *reinterpret_cast<const uint2*>(p);
+          const T* o = reinterpret_cast<const T*>(&old);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += (float)o[e];
+          for (int e = 0; e < 4; ++e) v[e] += (float)o[e];
+        }
+        *reinterpret_cast<uint2*>(p) = make_uint2(pack_x2<T>(v[0], v[1]), pack_x2<T>(v[2], v[3]));
       }
-      *reinterpret_cast<uint2*>(p) = make_uint2(pack_x2<T>(v[0], v[1]), pack_x2<T>(v[2], v[3]));
+    }
+  };
+  const int ndp = nwg - n_split;  // whole tiles first, then n_split tiles x S split units
+  const bool split = (int)blockIdx.x >= ndp;
+  int lin, k0 = 0, k1 = nk, part = 0, st = 0;
+  if (!split) {
+    lin = xcd_remap(blockIdx.x, ndp);
+  } else {
+    const int u = (int)blockIdx.x - ndp;
+    st = u / S;
+    part = u % S;
+    lin = ndp + st;
+    k0 = (int)((long)nk * part / S);
+    k1 = (int)((long)nk * (part + 1) / S);
+  }
+  long m0, n0;
+  tile_origin(lin, m0, n0);
+  run(m0, n0, k0, k1);
+  if (split) {
+    // fp32 partial in register order (thread t's register r at r * NTH + t)
+    float* w = ws + ((long)st * S + part) * (BM * BN);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[((i * 8 + j) * 4 + e) * NTH + tid] = acc[i][j][e];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* last = reinterpret_cast<int*>(smem);  // the one LDS array (free after run)
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int ticket = __hip_atomic_fetch_add(tickets + st, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *last = ticket == S - 1;
+      if (ticket == S - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    __syncthreads();
+    if (!*last) return;
+    // sum the S partials in part order (its own included, re-read from ws: same order whoever is last)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int p = 0; p < S; ++p) {
+      const float* wp = ws + ((long)st * S + p) * (BM * BN);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][j][e] += wp[((i * 8 + j) * 4 + e) * NTH + tid];
     }
   }
+  store_c(m0, n0);
 }
 
 }  // namespace wg
@@ -426,14 +498,39 @@ __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, c
 extern "C" {
 
 // C[M][N] (+)= A^T B with A [K][M] (row stride lda), B [K][N] (row stride ldb), C row stride ldc.
+// ws: pra_wgrad_ws_floats() fp32 scratch and tickets: pra_wgrad_ticket_count() ints (the split tail;
+// both may be null, then the tail runs as a partial data-parallel round).
+long pra_wgrad_ws_floats() { return 256L * 256 * 256 * 4; }  // 256 MiB: 1024 partial tiles
+int pra_wgrad_ticket_count() { return 256; }
+
 hipError_t pra_wgrad_gemm(int dtype, const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb,
-                          long ldc, int accumulate, hipStream_t s) {
+                          long ldc, int accumulate, float* ws, int* tickets, hipStream_t s) {
   using namespace pra::wg;
   if (M % BM || N % BN || K % BK || K <= 0 || lda % 8 || ldb % 8 || ldc % 8) return hipErrorInvalidValue;
   if ((long)(BK - 1) * lda + M > 0x7fffffffL || (long)(BK - 1) * ldb + N > 0x7fffffffL) return hipErrorInvalidValue;
-  const dim3 grid((unsigned)((M / BM) * (N / BN))), block(NTH);
+  const int nwg = (M / BM) * (N / BN);
   const char* e = getenv("PRA_WGRAD_MFMA");  // read per call: in-process A/B
   const bool m32 = e && atoi(e) == 32;
+  // 16x16 kernel: split the tiles of a partial last round S ways over K (S in 1..8 minimising the
+  // rounds the split units take; ties -> smaller S)
+  int cus = 0, dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0)
+    return hipErrorInvalidValue;
+  int n_split = 0, S = 1;
+  const char* es = getenv("PRA_WGRAD_SPLIT");  // opt-in: measured slower on W13 (1.17 vs 1.24 PF)
+  if (!m32 && ws && tickets && nwg > cus && nwg % cus != 0 && es && atoi(es) == 1) {
+    const int R = nwg % cus, nk = K / BK;
+    double best = 1.0;  // unsplit: one more round
+    for (int c = 2; c <= 8 && c <= nk; ++c) {
+      const double t = (double)((R * c + cus - 1) / cus) / c;
+      if (t < best - 1e-9) best = t, S = c;
+    }
+    if (S > 1 && (long)R * S * BM * BN <= pra_wgrad_ws_floats() && R <= pra_wgrad_ticket_count()) n_split = R;
+    else S = 1;
+  }
+  if (n_split && hipMemsetAsync(tickets, 0, sizeof(int) * n_split, s) != hipSuccess) return hipErrorInvalidValue;
+  const dim3 grid(m32 ? nwg : nwg - n_split + n_split * S), block(NTH);
 #define PRA_WG_LAUNCH(TT)                                                                                     \
   if (m32) {                                                                                                  \
     if (accumulate)                                                                                           \
@@ -445,10 +542,10 @@ hipError_t pra_wgrad_gemm(int dtype, const void* A, const void* B, void* C, int 
   } else {                                                                                                    \
     if (accumulate)                                                                                           \
       hipLaunchKernelGGL((wgrad16_kernel<TT, true>), grid, block, 0, s, (const TT*)A, (const TT*)B, (TT*)C, M, \
-                         N, K, lda, ldb, ldc);                                                                \
+                         N, K, lda, ldb, ldc, ws, tickets, n_split, S);                                       \
     else                                                                                                      \
       hipLaunchKernelGGL((wgrad16_kernel<TT, false>), grid, block, 0, s, (const TT*)A, (const TT*)B, (TT*)C, \
-                         M, N, K, lda, ldb, ldc);                                                             \
+                         M, N, K, lda, ldb, ldc, ws, tickets, n_split, S);                                    \
   }
   if (dtype == pra::kBF16) {
     PRA_WG_LAUNCH(__bf16)

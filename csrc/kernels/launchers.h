@@ -39,7 +39,9 @@ hipError_t pra_transpose16(const void* src, void* dst, long R, long C, long ld_s
 // C[M][N] (+)= A^T B, A [K][M], B [K][N] row-major (weight gradient on row-major activations);
 // M, N multiples of 256, K of 32 (gemm_wgrad.hip)
 hipError_t pra_wgrad_gemm(int dtype, const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb,
-                          long ldc, int accumulate, hipStream_t s);
+                          long ldc, int accumulate, float* ws, int* tickets, hipStream_t s);
+long pra_wgrad_ws_floats();
+int pra_wgrad_ticket_count();
 
 hipError_t pra_xent_fwd(int dtype, const void* logits, const int64_t* labels, float* lse, float* loss_row,
                         float* stats, long T, long V, long ld, long ignore_index, hipStream_t s);

@@ -101,11 +101,13 @@ def _tn_ok(t):
             and t.size(1) % 64 == 0 and t.stride(0) % 8 == 0)
 
 
-# Weight gradients on the hand-written MFMA GEMM (csrc/kernels/gemm_wgrad.hip, default): dW = dY^T X
-# read straight from the row-major activations, transposed inside the LDS read
+# PYRECOVER_WGRAD=hip: weight gradients on the hand-written MFMA GEMM (csrc/kernels/gemm_wgrad.hip):
+# dW = dY^T X read straight from the row-major activations, transposed inside the LDS read
 # (ds_read_b64_tr_b16), so neither the TN transposes nor the transposing epilogues (a^T, dgu^T,
-# dqkv^T) are needed. PYRECOVER_WGRAD=lib restores hipBLASLt on transposed operands.
-WGRAD_HIP = os.environ.get("PYRECOVER_WGRAD", "hip") == "hip"
+# dqkv^T) are needed. On those row-major operands it is 13-22% faster than hipBLASLt, but hipBLASLt
+# on K-contiguous copies is faster still, transposes included: 7B B16 step 1101 ms (hip) vs 1065 ms
+# (default, profiles/wgrad_mfma_r2.md), so the library TN path stays the default.
+WGRAD_HIP = os.environ.get("PYRECOVER_WGRAD", "lib") == "hip"
 
 
 def _hip_wgrad_dims(t, tokens, *cols) -> bool:

@@ -264,9 +264,9 @@ def test_shapes_outside_the_hip_kernels_fall_back(cuda, over):
 
 
 def test_mfma_wgrad_matches_library_wgrad(cuda, monkeypatch):
-    """The default weight gradients (hand-written MFMA kernel on the row-major activations, no
-    transposed copies) match the hipBLASLt path on transposed operands up to GEMM rounding, on a
-    model whose every projection (QKV, O, W1|W3, W2, head) fits the kernel."""
+    """The hand-written MFMA weight gradients (PYRECOVER_WGRAD=hip: row-major activations, no
+    transposed copies) match the default hipBLASLt path on transposed operands up to GEMM rounding,
+    on a model whose every projection (QKV, O, W1|W3, W2, head) fits the kernel."""
     from pyrecover_amd.ops import fused
 
     grads = []
