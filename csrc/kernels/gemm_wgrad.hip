@@ -42,6 +42,7 @@ template <typename T>
 using V8 = typename Elem<T>::v8;
 
 constexpr int BM = 256, BN = 256, BK = 32, TD = 256, NTH = 256, NS = 4;
+
 constexpr int TILE = BK * TD;                 // elements per staged operand tile (16 KiB)
 constexpr int NI = TILE * 2 / (NTH * 16);     // LDS-DMA instructions per lane per operand tile (4)
 
@@ -77,6 +78,17 @@ __device__ __forceinline__ uint32_t pack_x2(float a, float b) {
 
 template <int N>
 using IC = std::integral_constant<int, N>;
+
+// s_waitcnt vmcnt(N) for a compile-time N
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N == 0 || N == 8 || N == 16 || N == 24 || N == 32, "add the count");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  if constexpr (N == 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+}
 
 // one 16-B-per-lane LDS-DMA (global_load_lds_dwordx4): lane l's 16 bytes land at LDS byte
 // lds + 16 l (M0 = wave-uniform LDS base; one wait state between the M0 write and the load).
@@ -278,12 +290,13 @@ __device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
 // ws and takes a ticket; the last arriver of a tile sums the S partials in part order (its own from
 // ws too) -- deterministic, and nothing ever waits on another
 // workgroup.
-template <typename T, bool ACC>
+// NS16: ring depth (4 stages = 128 KiB, 5 = all 160 KiB of LDS)
+template <typename T, bool ACC, int NS16>
 __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, const T* __restrict__ B,
                                                       T* __restrict__ C, int M, int N, int K, long lda, long ldb,
                                                       long ldc, float* __restrict__ ws, int* __restrict__ tickets,
                                                       int n_split, int S) {
-  __shared__ __attribute__((aligned(1024))) T smem[NS * 2 * TILE];
+  __shared__ __attribute__((aligned(1024))) T smem[NS16 * 2 * TILE];
   const int tiles_m = M / BM, tiles_n = N / BN, nwg = tiles_m * tiles_n, nk = K / BK;
   // XCD-contiguous index of workgroup `orig` among n (undo the round-robin placement over the 8 XCDs)
   auto xcd_remap = [](int orig, int n) {
@@ -359,10 +372,10 @@ __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, c
     // every step issues exactly one stage of DMA (a stage past k1 re-loads stage k1 - 1 into the
     // slot nobody reads again), so the counted waits are the same on every step
 #pragma unroll
-    for (int p = 0; p < NS - 1; ++p)
+    for (int p = 0; p < NS16 - 1; ++p)
 #pragma unroll
       for (int u = 0; u < 2 * NI; ++u) dma(p, min(k0 + p, k1 - 1), u);
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    wait_vm<2 * NI * (NS16 - 2)>();  // stage k0 landed; the younger stages stay in flight
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 #pragma unroll
@@ -374,16 +387,16 @@ __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, c
     // publish stage kt + 1 and free the slot of stage kt - 1; m-blocks 4..7 in 8 groups of 4
     // MFMAs, each with 4 fragment reads of stage kt + 1 and one DMA instruction of stage kt + 3.
     auto step = [&](auto s_c, V8<T> (&ca)[8], V8<T> (&cb)[8], V8<T> (&na)[8], V8<T> (&nb)[8], int kt) {
-      constexpr int s = decltype(s_c)::value, sn = (s + 1) % NS, sd = (s + NS - 1) % NS;
+      constexpr int s = decltype(s_c)::value % NS16, sn = (s + 1) % NS16, sd = (s + NS16 - 1) % NS16;
       const T* nta = smem + sn * 2 * TILE;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[i][j] = mfma16(cb[j], ca[i], acc[i][j]);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      wait_vm<2 * NI * (NS16 - 3)>();  // stage kt + 1 landed
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      const int kd = min(kt + NS - 1, k1 - 1);
+      const int kd = min(kt + NS16 - 1, k1 - 1);
 #pragma unroll
       for (int gi = 0; gi < 8; ++gi) {
         na[gi] = fragA(nta, gi);
@@ -402,11 +415,23 @@ __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, c
         dma(sd, kd, gi);
       }
     };
-    for (int kt = k0; kt < k1; kt += NS) {
-      step(IC<0>{}, fa0, fb0, fa1, fb1, kt);
-      if (kt + 1 < k1) step(IC<1>{}, fa1, fb1, fa0, fb0, kt + 1);
-      if (kt + 2 < k1) step(IC<2>{}, fa0, fb0, fa1, fb1, kt + 2);
-      if (kt + 3 < k1) step(IC<3>{}, fa1, fb1, fa0, fb0, kt + 3);
+    // unrolled by lcm(NS16, 2): compile-time ring slot and fragment register set
+    static_assert(NS16 == 4 || NS16 == 5, "unroll below");
+    constexpr int UNR = NS16 == 4 ? 4 : 10;
+    for (int kt = k0; kt < k1; kt += UNR) {
+      auto st = [&](auto j_c) __attribute__((always_inline)) {
+        constexpr int j = decltype(j_c)::value;
+        if (kt + j < k1) {
+          if constexpr (j % 2 == 0)
+            step(IC<j>{}, fa0, fb0, fa1, fb1, kt + j);
+          else
+            step(IC<j>{}, fa1, fb1, fa0, fb0, kt + j);
+        }
+      };
+      st(IC<0>{}); st(IC<1>{}); st(IC<2>{}); st(IC<3>{});
+      if constexpr (UNR == 10) {
+        st(IC<4>{}); st(IC<5>{}); st(IC<6>{}); st(IC<7>{}); st(IC<8>{}); st(IC<9>{});
+      }
     }
     // no LDS-DMA may land after this point (next tile's prologue / end of the workgroup), and no
     // wave may still read a slot the next prologue overwrites
@@ -511,6 +536,8 @@ hipError_t pra_wgrad_gemm(int dtype, const void* A, const void* B, void* C, int 
   const int nwg = (M / BM) * (N / BN);
   const char* e = getenv("PRA_WGRAD_MFMA");  // read per call: in-process A/B
   const bool m32 = e && atoi(e) == 32;
+  const char* en = getenv("PRA_WGRAD_STAGES");  // 16x16 ring depth: 4 or 5 (default)
+  const bool ns5 = !(en && atoi(en) == 4);
   // 16x16 kernel: split the tiles of a partial last round S ways over K (S in 1..8 minimising the
   // rounds the split units take; ties -> smaller S)
   int cus = 0, dev = 0;
@@ -539,12 +566,19 @@ hipError_t pra_wgrad_gemm(int dtype, const void* A, const void* B, void* C, int 
     else                                                                                                      \
       hipLaunchKernelGGL((wgrad_kernel<TT, false>), grid, block, 0, s, (const TT*)A, (const TT*)B, (TT*)C, M, \
                          N, K, lda, ldb, ldc);                                                                \
+  } else if (ns5) {                                                                                           \
+    if (accumulate)                                                                                           \
+      hipLaunchKernelGGL((wgrad16_kernel<TT, true, 5>), grid, block, 0, s, (const TT*)A, (const TT*)B, (TT*)C,  \
+                         M, N, K, lda, ldb, ldc, ws, tickets, n_split, S);                                    \
+    else                                                                                                      \
+      hipLaunchKernelGGL((wgrad16_kernel<TT, false, 5>), grid, block, 0, s, (const TT*)A, (const TT*)B, (TT*)C, \
+                         M, N, K, lda, ldb, ldc, ws, tickets, n_split, S);                                    \
   } else {                                                                                                    \
     if (accumulate)                                                                                           \
-      hipLaunchKernelGGL((wgrad16_kernel<TT, true>), grid, block, 0, s, (const TT*)A, (const TT*)B, (TT*)C, M, \
-                         N, K, lda, ldb, ldc, ws, tickets, n_split, S);                                       \
+      hipLaunchKernelGGL((wgrad16_kernel<TT, true, 4>), grid, block, 0, s, (const TT*)A, (const TT*)B, (TT*)C,  \
+                         M, N, K, lda, ldb, ldc, ws, tickets, n_split, S);                                    \
     else                                                                                                      \
-      hipLaunchKernelGGL((wgrad16_kernel<TT, false>), grid, block, 0, s, (const TT*)A, (const TT*)B, (TT*)C, \
+      hipLaunchKernelGGL((wgrad16_kernel<TT, false, 4>), grid, block, 0, s, (const TT*)A, (const TT*)B, (TT*)C, \
                          M, N, K, lda, ldb, ldc, ws, tickets, n_split, S);                                    \
   }
   if (dtype == pra::kBF16) {

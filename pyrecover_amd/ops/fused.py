@@ -101,24 +101,41 @@ def _tn_ok(t):
             and t.size(1) % 64 == 0 and t.stride(0) % 8 == 0)
 
 
-# PYRECOVER_WGRAD=hip: weight gradients on the hand-written MFMA GEMM (csrc/kernels/gemm_wgrad.hip):
-# dW = dY^T X read straight from the row-major activations, transposed inside the LDS read
-# (ds_read_b64_tr_b16), so neither the TN transposes nor the transposing epilogues (a^T, dgu^T,
-# dqkv^T) are needed. On those row-major operands it is 13-22% faster than hipBLASLt, but hipBLASLt
-# on K-contiguous copies is faster still, transposes included: 7B B16 step 1101 ms (hip) vs 1065 ms
-# (default, profiles/wgrad_mfma_r2.md), so the library TN path stays the default.
-WGRAD_HIP = os.environ.get("PYRECOVER_WGRAD", "lib") == "hip"
+# Weight gradients on the hand-written MFMA GEMM (csrc/kernels/gemm_wgrad.hip): dW = dY^T X read
+# straight from the row-major activations, transposed inside the LDS read (ds_read_b64_tr_b16), so
+# that site needs neither the TN transposes nor a transposing epilogue. On those operands it is
+# 13-22% faster than hipBLASLt, but hipBLASLt on K-contiguous copies is faster per GEMM; the kernel
+# wins where the library path's copies cost the most (profiles/wgrad_mfma_r2.md).
+# PYRECOVER_WGRAD: "auto" (default: the sites where it wins in the step: the output projection,
+# whose library path transposes both operands, and the output head, whose dlogits^T copy is
+# T x vocab; 7B B16 31.03k vs 30.95k tok/s, profiles/wgrad_mfma_r2.md), "hip" (every site), "lib"
+# (none: hipBLASLt TN everywhere), or a comma list of sites (qkv, o, w13, w2, head).
+_WGRAD_SITE_SETS = {"lib": frozenset(), "hip": frozenset({"qkv", "o", "w13", "w2", "head"}),
+                    "auto": frozenset({"o", "head"})}
 
 
-def _hip_wgrad_dims(t, tokens, *cols) -> bool:
+def _wgrad_sites(v: str) -> frozenset:
+    if v in _WGRAD_SITE_SETS:
+        return _WGRAD_SITE_SETS[v]
+    sites = frozenset(x.strip() for x in v.split(",") if x.strip())
+    bad = sites - _WGRAD_SITE_SETS["hip"]
+    if bad:
+        raise ValueError(f"PYRECOVER_WGRAD: unknown site(s) {sorted(bad)}")
+    return sites
+
+
+WGRAD_SITES = _wgrad_sites(os.environ.get("PYRECOVER_WGRAD", "auto"))
+
+
+def _hip_wgrad_dims(t, site, tokens, *cols) -> bool:
     """The MFMA weight-gradient kernel's shape rules: K = tokens % 32, every output dim % 256."""
-    return (WGRAD_HIP and _ext.hip16(t) and tokens % 32 == 0 and tokens > 0
+    return (site in WGRAD_SITES and _ext.hip16(t) and tokens % 32 == 0 and tokens > 0
             and all(c % 256 == 0 for c in cols))
 
 
-def _hip_wgrad_ok(dy2, x2) -> bool:
+def _hip_wgrad_ok(dy2, x2, site) -> bool:
     return (dy2.dim() == 2 and x2.dim() == 2 and dy2.dtype == x2.dtype and dy2.device == x2.device
-            and dy2.size(0) == x2.size(0) and _hip_wgrad_dims(dy2, dy2.size(0), dy2.size(1), x2.size(1))
+            and dy2.size(0) == x2.size(0) and _hip_wgrad_dims(dy2, site, dy2.size(0), dy2.size(1), x2.size(1))
             and all(t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0 for t in (dy2, x2)))
 
 
@@ -134,9 +151,9 @@ def _hip_wgrad(slot, dy2, x2, shape):
         slot.end(buf)
 
 
-def _wgrad_into(slot, dy2, x2, shape):
-    """slot <- dy2^T x2 (dy2 [T, out], x2 [T, in])."""
-    if _hip_wgrad_ok(dy2, x2):
+def _wgrad_into(slot, dy2, x2, shape, site):
+    """slot <- dy2^T x2 (dy2 [T, out], x2 [T, in]); `site` names the projection (WGRAD_SITES)."""
+    if _hip_wgrad_ok(dy2, x2, site):
         _hip_wgrad(slot, dy2, x2, shape)
     elif TN_WGRAD and _tn_ok(dy2) and _tn_ok(x2):
         C = _ext.require_for(dy2)
@@ -355,7 +372,7 @@ class _AttentionBlock(torch.autograd.Function):
         w_qkv_t, w_o_t = ctx.w_t if ctx.w_t is not None else (None, None)
         do = (torch.mm(dy2, w_o_t.t()) if w_o_t is not None else torch.mm(dy2, w_o)).view(B, S, Hq, D)
         if TN_WGRAD_WO:
-            _wgrad_into(slot_o, dy2, o2, tuple(w_o.shape))  # TN: 0.53 -> ~0.3 ms + two 50-us transposes
+            _wgrad_into(slot_o, dy2, o2, tuple(w_o.shape), "o")
         else:
             slot_o.mm_(dy2.t(), o2, tuple(w_o.shape))
         dqkv = torch.empty_like(qkv)
@@ -366,7 +383,7 @@ class _AttentionBlock(torch.autograd.Function):
         dk = dqkv[:, nq:nq + nk].view(B, S, Hkv, D)
         dv = dqkv[:, nq + nk:].view(B, S, Hkv, D)
         _attn_bwd(q, k, v, o, do, lse, dq, dk, dv, ctx.scale, causal)
-        if (not _hip_wgrad_ok(dqkv, x2) and TN_WGRAD and _tn_ok(dqkv) and _tn_ok(x2) and T % S == 0
+        if (not _hip_wgrad_ok(dqkv, x2, "qkv") and TN_WGRAD and _tn_ok(dqkv) and _tn_ok(x2) and T % S == 0
                 and D % 8 == 0):
             # inverse RoPE in place + dqkv^T in one pass, for the K-contiguous weight-grad GEMM
             C = _ext.require_for(dqkv)
@@ -379,7 +396,7 @@ class _AttentionBlock(torch.autograd.Function):
             else:
                 ref.rope_inplace_2d(dqkv, nq + nk, tab, D, S, inverse=True)
             dx = torch.mm(dqkv, w_qkv_t.t()) if w_qkv_t is not None else torch.mm(dqkv, w_qkv)
-            _wgrad_into(slot_qkv, dqkv, x2, tuple(w_qkv.shape))
+            _wgrad_into(slot_qkv, dqkv, x2, tuple(w_qkv.shape), "qkv")
         n_params = ctx.needs_input_grad.__len__() - 8
         return (dx.view(B, S, -1), None, None, None, None, None, None, None) + (None,) * n_params
 
@@ -419,7 +436,7 @@ class _SwiGLUMLP(torch.autograd.Function):
         x2 = x.reshape(-1, shape[-1])
         gu = torch.mm(x2, w13.t())
         F = gu.shape[1] // 2
-        if (not _hip_wgrad_dims(gu, gu.shape[0], shape[-1], F) and TN_WGRAD and _tn_ok(gu)
+        if (not _hip_wgrad_dims(gu, "w2", gu.shape[0], shape[-1], F) and TN_WGRAD and _tn_ok(gu)
                 and F % 64 == 0):
             # a^T (K-contiguous operand of the W2 weight gradient) is written in the same pass and
             # kept instead of a
@@ -445,8 +462,8 @@ class _SwiGLUMLP(torch.autograd.Function):
             dyT = _ext.require_for(dy2).transpose2d(dy2) if _tn_ok(dy2) else dy2.t()
             slot2.mm_(dyT, a.t(), tuple(w2.shape))
         else:
-            _wgrad_into(slot2, dy2, a, tuple(w2.shape))
-        if _hip_wgrad_ok(gu, x2):
+            _wgrad_into(slot2, dy2, a, tuple(w2.shape), "w2")
+        if _hip_wgrad_ok(gu, x2, "w13"):
             dgu = _swiglu_bwd_(da, gu)  # in place over gu; no transposed copy for the MFMA wgrad
             dx = torch.mm(dgu, w13_t.t()) if w13_t is not None else torch.mm(dgu, w13)
             _hip_wgrad(slot13, dgu, x2, tuple(w13.shape))
@@ -459,7 +476,7 @@ class _SwiGLUMLP(torch.autograd.Function):
         else:
             dgu = _swiglu_bwd_(da, gu)  # in place over gu (dead after this)
             dx = torch.mm(dgu, w13_t.t()) if w13_t is not None else torch.mm(dgu, w13)
-            _wgrad_into(slot13, dgu, x2, tuple(w13.shape))
+            _wgrad_into(slot13, dgu, x2, tuple(w13.shape), "w13")
         n_params = len(ctx.needs_input_grad) - 6
         return (dx.view(shape), None, None, None, None, None) + (None,) * n_params
 
@@ -509,7 +526,7 @@ class _LinearCrossEntropy(torch.autograd.Function):
             p = p * valid.to(p.dtype).unsqueeze(1) * (dloss.to(p.dtype) / n)
             dlogits = p.to(logits.dtype)
         dh = torch.mm(dlogits, ctx.w_t.t()) if ctx.w_t is not None else torch.mm(dlogits, w_out)
-        _wgrad_into(ctx.slot, dlogits, h2, tuple(w_out.shape))
+        _wgrad_into(ctx.slot, dlogits, h2, tuple(w_out.shape), "head")
         return dh.view(ctx.hshape), None, None, None, None, None, None
 
 

@@ -415,7 +415,7 @@ def test_adamw_t_matches_flat_adamw_plus_transpose(cuda, monkeypatch, strip, row
 
 # ---------------------------------------------------------------------------------------
 # Weight-gradient MFMA GEMM (csrc/kernels/gemm_wgrad.hip): out (+)= a^T b on row-major operands
-@pytest.mark.parametrize("mfma", ["16", "32"])
+@pytest.mark.parametrize("mfma", ["16", "32", "16s4"])
 @pytest.mark.parametrize("K,M,N,dtype", [(32, 256, 256, torch.bfloat16), (2048, 768, 512, torch.bfloat16),
                                          (4096, 512, 1024, torch.float16), (96, 1280, 256, torch.bfloat16),
                                          # 300 tiles on 256 CUs: 44 tail tiles split over K
@@ -423,7 +423,8 @@ def test_adamw_t_matches_flat_adamw_plus_transpose(cuda, monkeypatch, strip, row
 @pytest.mark.parametrize("accumulate", [False, True])
 @pytest.mark.parametrize("split", ["0", "1"])
 def test_wgrad_mm_vs_fp32(cuda, monkeypatch, mfma, K, M, N, dtype, accumulate, split):
-    monkeypatch.setenv("PRA_WGRAD_MFMA", mfma)
+    monkeypatch.setenv("PRA_WGRAD_MFMA", mfma[:2])
+    monkeypatch.setenv("PRA_WGRAD_STAGES", "4" if mfma == "16s4" else "5")
     monkeypatch.setenv("PRA_WGRAD_SPLIT", split)
     C_ = _ext.native()
     g = torch.Generator(device=cuda)

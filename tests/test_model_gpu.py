@@ -264,14 +264,15 @@ def test_shapes_outside_the_hip_kernels_fall_back(cuda, over):
 
 
 def test_mfma_wgrad_matches_library_wgrad(cuda, monkeypatch):
-    """The hand-written MFMA weight gradients (PYRECOVER_WGRAD=hip: row-major activations, no
-    transposed copies) match the default hipBLASLt path on transposed operands up to GEMM rounding,
-    on a model whose every projection (QKV, O, W1|W3, W2, head) fits the kernel."""
+    """The hand-written MFMA weight gradients at every site (PYRECOVER_WGRAD=hip: row-major
+    activations, no transposed copies) match hipBLASLt on transposed operands at every site
+    (=lib) up to GEMM rounding, on a model whose every projection (QKV, O, W1|W3, W2, head) fits
+    the kernel."""
     from pyrecover_amd.ops import fused
 
     grads = []
-    for hip in (True, False):
-        monkeypatch.setattr(fused, "WGRAD_HIP", hip)
+    for sites in ("hip", "lib"):
+        monkeypatch.setattr(fused, "WGRAD_SITES", fused._WGRAD_SITE_SETS[sites])
         torch.manual_seed(0)
         a = get_preset("llama-tiny", seq_len=256, multiple_of=256)
         prev = torch.get_default_dtype()

@@ -38,8 +38,9 @@ def main():
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     # correctness: fp32 reference on a short K, plain and accumulate, both MFMA shapes
-    for (name, M, N), mf in [(sh, mf) for sh in SHAPES for mf in ("16", "32")]:
-        os.environ["PRA_WGRAD_MFMA"] = mf
+    for (name, M, N), mf in [(sh, mf) for sh in SHAPES for mf in ("16", "32", "16s4")]:
+        os.environ["PRA_WGRAD_MFMA"] = mf[:2]
+        os.environ["PRA_WGRAD_STAGES"] = "4" if mf == "16s4" else "5"
         K = 512
         dy = torch.randn(K, M, device=dev).bfloat16()
         x = torch.randn(K, N, device=dev).bfloat16()
@@ -54,6 +55,7 @@ def main():
         print(json.dumps({"check": name, "mfma": mf, "rel_err": err, "rel_err_acc": err2}), flush=True)
         assert err < 1e-2 and err2 < 1e-2, (name, err, err2)
     del os.environ["PRA_WGRAD_MFMA"]
+    del os.environ["PRA_WGRAD_STAGES"]
     T = args.tokens
     sel = set(args.shapes.split(",")) if args.shapes else None
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -71,7 +73,13 @@ def main():
             "tn+T": lambda: torch.mm(C.transpose2d(dy, dyT), C.transpose2d(x, xT).t(), out=out),
             "hip": lambda: C.wgrad_mm_(dy, x, out, False),
             "hip32": lambda: hip32(),
+            "hip_ns4": lambda: hip_ns4(),
         }
+
+        def hip_ns4():
+            os.environ["PRA_WGRAD_STAGES"] = "4"
+            C.wgrad_mm_(dy, x, out, False)
+            del os.environ["PRA_WGRAD_STAGES"]
 
         def hip32():
             os.environ["PRA_WGRAD_MFMA"] = "32"
