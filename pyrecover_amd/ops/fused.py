@@ -106,10 +106,11 @@ def _tn_ok(t):
 # that site needs neither the TN transposes nor a transposing epilogue. On those operands it is
 # 13-22% faster than hipBLASLt, but hipBLASLt on K-contiguous copies is faster per GEMM; the kernel
 # wins where the library path's copies cost the most (profiles/wgrad_mfma_r2.md).
-# PYRECOVER_WGRAD: "auto" (default: the sites where it wins in the step: the output projection,
-# whose library path transposes both operands, and the output head, whose dlogits^T copy is
-# T x vocab; 7B B16 31.03k vs 30.95k tok/s, profiles/wgrad_mfma_r2.md), "hip" (every site), "lib"
-# (none: hipBLASLt TN everywhere), or a comma list of sites (qkv, o, w13, w2, head).
+# PYRECOVER_WGRAD: "auto" (default: the sites where it wins in the step, at >= 16384 tokens per
+# GEMM: the output projection, whose library path transposes both operands, and the output head,
+# whose dlogits^T copy is T x vocab; 7B B16 31.03k vs 30.95k tok/s, but Llama-3-8B S8192 B1 (8192
+# tokens) -0.2%, profiles/wgrad_mfma_r2.md), "hip" (every site), "lib" (none: hipBLASLt TN
+# everywhere), or a comma list of sites (qkv, o, w13, w2, head).
 _WGRAD_SITE_SETS = {"lib": frozenset(), "hip": frozenset({"qkv", "o", "w13", "w2", "head"}),
                     "auto": frozenset({"o", "head"})}
 
@@ -125,12 +126,14 @@ def _wgrad_sites(v: str) -> frozenset:
 
 
 WGRAD_SITES = _wgrad_sites(os.environ.get("PYRECOVER_WGRAD", "auto"))
+WGRAD_AUTO = os.environ.get("PYRECOVER_WGRAD", "auto") == "auto"
+WGRAD_AUTO_MIN_TOKENS = 16384
 
 
 def _hip_wgrad_dims(t, site, tokens, *cols) -> bool:
     """The MFMA weight-gradient kernel's shape rules: K = tokens % 32, every output dim % 256."""
     return (site in WGRAD_SITES and _ext.hip16(t) and tokens % 32 == 0 and tokens > 0
-            and all(c % 256 == 0 for c in cols))
+            and (not WGRAD_AUTO or tokens >= WGRAD_AUTO_MIN_TOKENS) and all(c % 256 == 0 for c in cols))
 
 
 def _hip_wgrad_ok(dy2, x2, site) -> bool:
