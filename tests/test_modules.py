@@ -83,3 +83,21 @@ def test_module_forwards_on_gpu(cuda):
     _check(m.layers["0"].feed_forward.to(cuda, torch.bfloat16), lambda mod, t: mod(t), ref_ff, x, 3e-2)
     _check(m.layers["1"].to(cuda, torch.bfloat16), lambda mod, t: mod(t, fc),
            lambda mod, t: ref_block(mod, t, fc.cpu()), x, 3e-2)
+
+
+def test_wgrad_site_selection_parsing():
+    """PYRECOVER_WGRAD: named sets, comma lists of sites, unknown sites rejected; the CPU path
+    never selects the HIP weight-gradient kernel."""
+    import pytest
+    import torch
+
+    from pyrecover_amd.ops import fused
+
+    assert fused._wgrad_sites("lib") == frozenset()
+    assert fused._wgrad_sites("auto") == frozenset({"o", "head"})
+    assert fused._wgrad_sites("hip") == frozenset({"qkv", "o", "w13", "w2", "head"})
+    assert fused._wgrad_sites("o, qkv") == frozenset({"o", "qkv"})
+    with pytest.raises(ValueError):
+        fused._wgrad_sites("o,attn")
+    x = torch.zeros(32768, 256, dtype=torch.bfloat16)
+    assert not fused._hip_wgrad_ok(x, x, "o")
