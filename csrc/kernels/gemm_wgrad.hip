@@ -79,6 +79,13 @@ __device__ __forceinline__ uint32_t pack_x2(float a, float b) {
 template <int N>
 using IC = std::integral_constant<int, N>;
 
+// the same with a wave-uniform 64-bit base in SGPRs and a per-lane 32-bit byte offset ("saddr"
+// form): no per-instruction 64-bit VALU address add
+__device__ __forceinline__ void dma16s(const void* sbase, uint32_t voff, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds)
+               : "memory");
+}
+
 // s_waitcnt vmcnt(N) for a compile-time N
 template <int N>
 __device__ __forceinline__ void wait_vm() {
@@ -314,15 +321,16 @@ __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, c
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
 
-  int offa[NI], offb[NI];
+  uint32_t offa[NI], offb[NI];  // per-lane byte offsets of the DMA sources within a stage
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     int r, ch;
     lay_inverse(((i * 4 + wid) * 64 + lane) * 16, r, ch);
-    offa[i] = r * (int)lda + ch * 8;
-    offb[i] = r * (int)ldb + ch * 8;
+    offa[i] = (uint32_t)((r * (int)lda + ch * 8) * (int)sizeof(T));
+    offb[i] = (uint32_t)((r * (int)ldb + ch * 8) * (int)sizeof(T));
   }
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) T*)smem;
+  const uint32_t ldsw = __builtin_amdgcn_readfirstlane(lds0 + wid * 1024);  // this wave's DMA base
 
   // lane offsets of the transposed reads: [column-block parity][lo/hi]
   int oa[2][2], ob[2][2];
@@ -363,11 +371,12 @@ __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, c
       for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     const T* Ab = A + m0;
     const T* Bb = B + n0;
-    auto dma = [&](int s, int kt, int u) __attribute__((always_inline)) {  // DMA instruction u (0..2NI-1) of stage kt into slot s
+    // DMA instruction u (0..2NI-1) of stage kt into slot s: SGPR base + per-lane byte offset
+    auto dma = [&](int s, int kt, int u) __attribute__((always_inline)) {
       const int i = u >> 1;
-      const uint32_t base = lds0 + (uint32_t)(s * 2 * TILE + (u & 1) * TILE) * sizeof(T);
-      const T* g = (u & 1) ? Bb + (long)kt * BK * ldb + offb[i] : Ab + (long)kt * BK * lda + offa[i];
-      dma16(g, __builtin_amdgcn_readfirstlane(base + (i * 4 + wid) * 1024));
+      const uint32_t lds = ldsw + (uint32_t)((s * 2 * TILE + (u & 1) * TILE) * sizeof(T) + i * 4 * 1024);
+      const T* g = (u & 1) ? Bb + (long)kt * BK * ldb : Ab + (long)kt * BK * lda;
+      dma16s(g, (u & 1) ? offb[i] : offa[i], lds);
     };
     // every step issues exactly one stage of DMA (a stage past k1 re-loads stage k1 - 1 into the
     // slot nobody reads again), so the counted waits are the same on every step
