@@ -547,18 +547,21 @@ hipError_t pra_wgrad_gemm(int dtype, const void* A, const void* B, void* C, int 
   const bool m32 = e && atoi(e) == 32;
   const char* en = getenv("PRA_WGRAD_STAGES");  // 16x16 ring depth: 4 or 5 (default)
   const bool ns5 = !(en && atoi(en) == 4);
-  // 16x16 kernel: split the tiles of a partial last round S ways over K (S in 1..8 minimising the
-  // rounds the split units take; ties -> smaller S)
+  // 16x16 kernel: split the tiles of a partial last round S ways over K (S in 1..2 minimising the
+  // rounds the split units take; ties -> smaller S). 7B shapes: W13 (96 tail tiles, S = 2) 1.29 ->
+  // 1.37 PF; W2 (176 tail tiles) would need S = 4, measured slower (1.36 -> 1.25 PF), so unsplit.
   int cus = 0, dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       cus <= 0)
     return hipErrorInvalidValue;
   int n_split = 0, S = 1;
-  const char* es = getenv("PRA_WGRAD_SPLIT");  // opt-in: measured slower on W13 (1.17 vs 1.24 PF)
-  if (!m32 && ws && tickets && nwg > cus && nwg % cus != 0 && es && atoi(es) == 1) {
+  const char* es = getenv("PRA_WGRAD_SPLIT");  // 0 disables the split tail
+  if (!m32 && ws && tickets && nwg > cus && nwg % cus != 0 && !(es && atoi(es) == 0)) {
     const int R = nwg % cus, nk = K / BK;
     double best = 1.0;  // unsplit: one more round
-    for (int c = 2; c <= 8 && c <= nk; ++c) {
+    const char* esm = getenv("PRA_WGRAD_SPLIT_MAX");  // largest split considered (default 2)
+    const int smax = esm ? atoi(esm) : 2;
+    for (int c = 2; c <= smax && c <= 8 && c <= nk; ++c) {
       const double t = (double)((R * c + cus - 1) / cus) / c;
       if (t < best - 1e-9) best = t, S = c;
     }

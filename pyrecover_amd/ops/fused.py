@@ -106,14 +106,16 @@ def _tn_ok(t):
 # that site needs neither the TN transposes nor a transposing epilogue. On those operands it is
 # 13-22% faster than hipBLASLt, but hipBLASLt on K-contiguous copies is faster per GEMM; the kernel
 # wins where the library path's copies cost the most (profiles/wgrad_mfma_r2.md).
-# PYRECOVER_WGRAD: "auto" (default: the sites where it wins in the step, at >= 16384 tokens per
-# GEMM: the output projection, whose library path transposes both operands, the QKV projection,
-# whose library path needs x^T and the transposing inverse-RoPE epilogue, and the output head,
-# whose dlogits^T copy is T x vocab; 7B B16 +0.5% over hipBLASLt TN at every site, but Llama-3-8B
-# S8192 B1 (8192 tokens) -0.2%, profiles/wgrad_mfma_r2.md), "hip" (every site), "lib" (none:
-# hipBLASLt TN everywhere), or a comma list of sites (qkv, o, w13, w2, head).
+# PYRECOVER_WGRAD: "auto" (default: the sites where it wins or ties in the step, at >= 16384
+# tokens per GEMM: the output projection, whose library path transposes both operands, QKV, whose
+# library path needs x^T and the transposing inverse-RoPE epilogue, W1|W3, whose library path needs
+# x^T and the transposing SwiGLU-backward epilogue, and the output head, whose dlogits^T copy is
+# T x vocab; W2 stays on hipBLASLt TN (-0.5% on the kernel). 7B B16 31.04k vs 30.95k tok/s with
+# hipBLASLt TN at every site; Llama-3-8B S8192 B1 (8192 tokens) -0.2%, hence the threshold.
+# profiles/wgrad_mfma_r2.md), "hip" (every site), "lib" (none), or a comma list of sites
+# (qkv, o, w13, w2, head).
 _WGRAD_SITE_SETS = {"lib": frozenset(), "hip": frozenset({"qkv", "o", "w13", "w2", "head"}),
-                    "auto": frozenset({"qkv", "o", "head"})}
+                    "auto": frozenset({"qkv", "o", "w13", "head"})}
 
 
 def _wgrad_sites(v: str) -> frozenset:

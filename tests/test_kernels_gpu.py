@@ -426,6 +426,7 @@ def test_wgrad_mm_vs_fp32(cuda, monkeypatch, mfma, K, M, N, dtype, accumulate, s
     monkeypatch.setenv("PRA_WGRAD_MFMA", mfma[:2])
     monkeypatch.setenv("PRA_WGRAD_STAGES", "4" if mfma == "16s4" else "5")
     monkeypatch.setenv("PRA_WGRAD_SPLIT", split)
+    monkeypatch.setenv("PRA_WGRAD_SPLIT_MAX", "8")  # exercise every split factor the search allows
     C_ = _ext.native()
     g = torch.Generator(device=cuda)
     g.manual_seed(K + M + N)

@@ -94,7 +94,7 @@ def test_wgrad_site_selection_parsing():
     from pyrecover_amd.ops import fused
 
     assert fused._wgrad_sites("lib") == frozenset()
-    assert fused._wgrad_sites("auto") == frozenset({"qkv", "o", "head"})
+    assert fused._wgrad_sites("auto") == frozenset({"qkv", "o", "w13", "head"})
     assert fused._wgrad_sites("hip") == frozenset({"qkv", "o", "w13", "w2", "head"})
     assert fused._wgrad_sites("o, qkv") == frozenset({"o", "qkv"})
     with pytest.raises(ValueError):

@@ -74,7 +74,13 @@ def main():
             "hip": lambda: C.wgrad_mm_(dy, x, out, False),
             "hip32": lambda: hip32(),
             "hip_ns4": lambda: hip_ns4(),
+            "hip_nosplit": lambda: hip_nosplit(),
         }
+
+        def hip_nosplit():
+            os.environ["PRA_WGRAD_SPLIT"] = "0"
+            C.wgrad_mm_(dy, x, out, False)
+            del os.environ["PRA_WGRAD_SPLIT"]
 
         def hip_ns4():
             os.environ["PRA_WGRAD_STAGES"] = "4"
