@@ -474,9 +474,12 @@ __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, c
   if (!split) {
     lin = xcd_remap(blockIdx.x, ndp);
   } else {
-    const int u = (int)blockIdx.x - ndp;
-    st = u / S;
-    part = u % S;
+    // part-major, XCD-contiguous: the units resident together on one XCD are consecutive tiles
+    // (group-M order) of the SAME K range, so they share A/B panel slices in L2 like the
+    // data-parallel rounds (W13 at S = 2: 1.37 -> 1.40 PF over tile-major order)
+    const int u = xcd_remap((int)blockIdx.x - ndp, n_split * S);
+    part = u / n_split;
+    st = u % n_split;
     lin = ndp + st;
     k0 = (int)((long)nk * part / S);
     k1 = (int)((long)nk * (part + 1) / S);
@@ -548,8 +551,8 @@ hipError_t pra_wgrad_gemm(int dtype, const void* A, const void* B, void* C, int 
   const char* en = getenv("PRA_WGRAD_STAGES");  // 16x16 ring depth: 4 or 5 (default)
   const bool ns5 = !(en && atoi(en) == 4);
   // 16x16 kernel: split the tiles of a partial last round S ways over K (S in 1..2 minimising the
-  // rounds the split units take; ties -> smaller S). 7B shapes: W13 (96 tail tiles, S = 2) 1.29 ->
-  // 1.37 PF; W2 (176 tail tiles) would need S = 4, measured slower (1.36 -> 1.25 PF), so unsplit.
+  // rounds the split units take; ties -> smaller S). 7B shapes: W13 (96 tail tiles, S = 2) 1.31 ->
+  // 1.40 PF; W2 (176 tail tiles) would need S = 4, measured slower (1.39 -> 1.24 PF), so unsplit.
   int cus = 0, dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       cus <= 0)
