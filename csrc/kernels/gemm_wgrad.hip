@@ -529,6 +529,12 @@ __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, c
   store_c(m0, n0);
 }
 
+// zeroes the split tail's tickets (a kernel node, ordered before the GEMM in a captured graph)
+__global__ __launch_bounds__(256) void zero_i32_kernel(int* __restrict__ p, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) p[i] = 0;
+}
+
 }  // namespace wg
 }  // namespace pra
 
@@ -571,7 +577,10 @@ hipError_t pra_wgrad_gemm(int dtype, const void* A, const void* B, void* C, int 
     if (S > 1 && (long)R * S * BM * BN <= pra_wgrad_ws_floats() && R <= pra_wgrad_ticket_count()) n_split = R;
     else S = 1;
   }
-  if (n_split && hipMemsetAsync(tickets, 0, sizeof(int) * n_split, s) != hipSuccess) return hipErrorInvalidValue;
+  // tickets are zeroed by a kernel, not hipMemsetAsync: replayed from a captured HIP graph
+  // (train.py --compile), the memset node's zeros were not seen by the GEMM's ticket atomics and
+  // most split tiles were never reduced (tests/test_kernels_gpu.py, graph-capture test)
+  if (n_split) hipLaunchKernelGGL(zero_i32_kernel, dim3((n_split + 255) / 256), dim3(256), 0, s, tickets, n_split);
   const dim3 grid(m32 ? nwg : nwg - n_split + n_split * S), block(NTH);
 #define PRA_WG_LAUNCH(TT)                                                                                     \
   if (m32) {                                                                                                  \

@@ -466,3 +466,32 @@ def test_wgrad_mm_rejects_bad_shapes(cuda):
     b = torch.randn(64, 256, device=cuda).bfloat16()
     with pytest.raises(RuntimeError):
         C_.wgrad_mm_(a, b, torch.empty(300, 256, device=cuda, dtype=torch.bfloat16), False)
+
+
+def test_wgrad_mm_split_tail_under_hip_graph_capture(cuda):
+    """The split tail's ticket memset and workspace are captured into a HIP graph (train.py
+    --compile); replays are bit-identical to eager calls, including after the inputs change."""
+    C_ = _ext.native()
+    torch.manual_seed(5)
+    K, M, N = 1024, 7680, 2560  # 300 tiles: 44 tail tiles split over K
+    a = torch.randn(K, M, device=cuda).bfloat16()
+    b = torch.randn(K, N, device=cuda).bfloat16()
+    out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    s = torch.cuda.Stream(cuda)
+    s.wait_stream(torch.cuda.current_stream(cuda))
+    with torch.cuda.stream(s):
+        C_.wgrad_mm_(a, b, out, False)  # warm-up outside capture
+    torch.cuda.current_stream(cuda).wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        C_.wgrad_mm_(a, b, out, False)
+    for _ in range(2):
+        a.copy_(torch.randn(K, M, device=cuda).bfloat16())
+        g.replay()
+        torch.cuda.synchronize()
+        ref = torch.empty_like(out)
+        C_.wgrad_mm_(a, b, ref, False)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
+    exact = a.float().t() @ b.float()
+    assert ((out.float() - exact).norm() / exact.norm()).item() < 5e-3
