@@ -68,10 +68,22 @@ def local_rank() -> int:
 
 
 def gpu_index(lrank: int) -> int:
-    """GPU of a local rank: one process per GPU. ``PYRECOVER_LOCAL_DEVICE=<i>`` pins every rank to
-    GPU i (rehearsing the multi-rank path on one GPU; use with PYRECOVER_DIST_BACKEND=gloo)."""
+    """Visible GPU of a local rank (one process per GPU).
+
+    * ``PYRECOVER_LOCAL_DEVICE=<i>`` pins every rank to GPU i (rehearsing the multi-rank path on
+      one GPU; use with PYRECOVER_DIST_BACKEND=gloo).
+    * One visible device (SLURM per-task isolation: ``--gpus-per-task=1`` / ``--gpu-bind``, or
+      ROCR/HIP_VISIBLE_DEVICES set per rank): device 0, whatever SLURM_LOCALID says.
+    * Otherwise every node GPU is visible, as in reference dist_utils.py:47,55: ``lrank % count``.
+
+    ``torch.cuda.device_count()`` does not initialise the GPU on this image."""
     o = os.environ.get("PYRECOVER_LOCAL_DEVICE")
-    return int(o) if o not in (None, "") else lrank
+    if o not in (None, ""):
+        return int(o)
+    n = torch.cuda.device_count() if torch.cuda.is_available() else 0
+    if n <= 0:
+        return lrank
+    return 0 if n == 1 else lrank % n
 
 
 def rccl_pg_options():
@@ -106,18 +118,22 @@ def maybe_init_distributed(activate_distributed: bool, backend: Optional[str] = 
     use_gpu = torch.cuda.is_available()
     if backend is None:
         backend = os.environ.get("PYRECOVER_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")  # nccl = RCCL
+    dev_index = gpu_index(lrank)
     if use_gpu:
-        torch.cuda.set_device(gpu_index(lrank))
+        torch.cuda.set_device(dev_index)
     if not torch.distributed.is_initialized():
         kw = {}
         if backend == "nccl":
-            kw["device_id"] = torch.device("cuda", gpu_index(lrank))
+            kw["device_id"] = torch.device("cuda", dev_index)
             opts = rccl_pg_options()
             if opts is not None:
                 kw["pg_options"] = opts
         torch.distributed.init_process_group(backend=backend, rank=rank, world_size=world,
                                              timeout=datetime.timedelta(seconds=timeout_s), **kw)
     _STATE.update(rank=rank, world=world, local_rank=lrank, initialized=True, backend=backend)
+    # every rank, like reference dist_utils.py:56-59 (plus the bound device)
+    print(f"[Rank {rank}] world_size={world}, local_rank={lrank}, "
+          f"device={'cuda:%d' % dev_index if use_gpu else 'cpu'}, pid={os.getpid()}", flush=True)
     log_rank0(f"Distributed initialized: backend={backend} world_size={world} rank={rank} local_rank={lrank}")
     return lrank, world
 

@@ -126,18 +126,45 @@ class XgmiAllReduce:
         di = self.dev.index
         self.dtype = flat.grad.dtype
         self.esz = flat.grad.element_size()
-        # 1) exportable gradient buffer
+        # 1) CPU barriers for the comm thread (its own gloo group, used by nothing else)
+        self.hgroup = dist.new_group(backend="gloo")
+        # 2) every peer GPU must be visible to map its buffer: under SLURM per-task isolation
+        # (--gpus-per-task=1 / --gpu-bind) each rank sees one device and peer IPC cannot work.
+        # Decided collectively, so every rank raises instead of one rank hanging the others.
+        n_vis = torch.cuda.device_count()
+        vis: List = [None] * W
+        dist.all_gather_object(vis, n_vis, group=self.hgroup)
+        if min(vis) < W:
+            raise RuntimeError(
+                f"xgmi all-reduce needs all {W} node GPUs visible to every rank (visible per rank: {vis}); "
+                "per-task GPU isolation (srun --gpus-per-task=1 / --gpu-bind, or per-rank "
+                "ROCR_VISIBLE_DEVICES) hides the peers. Use the default RCCL all-reduce "
+                "(--allreduce rccl) or launch with every GPU visible.")
+        # 3) exportable gradient buffer
         buf = self.C.ipc_empty(flat.grad.numel(), self.dtype, di)
         buf.copy_(flat.grad)
         flat.rebind_grad(buf)
         self.buf = buf
-        # 2) CPU barriers for the comm thread (its own gloo group, used by nothing else)
-        self.hgroup = dist.new_group(backend="gloo")
-        # 3) peer buffers
+        # 4) peer buffers (a failed open is reported on every rank)
         handles: List = [None] * W
         dist.all_gather_object(handles, self.C.ipc_mem_handle(buf), group=self.hgroup)
         base = buf.data_ptr()
-        self.peer_base = [base if r == self.rank else self.C.ipc_open_mem(handles[r], di) for r in range(W)]
+        self.peer_base, err = [], None
+        for r in range(W):
+            if r == self.rank:
+                self.peer_base.append(base)
+                continue
+            try:
+                self.peer_base.append(self.C.ipc_open_mem(handles[r], di))
+            except RuntimeError as e:  # noqa: PERF203
+                err = f"rank {self.rank}: ipc_open_mem of rank {r}'s buffer failed: {e}"
+                break
+        errs: List = [None] * W
+        dist.all_gather_object(errs, err, group=self.hgroup)
+        bad = [e for e in errs if e]
+        if bad:
+            raise RuntimeError("xgmi all-reduce cannot map peer gradient buffers (GPU isolation or no "
+                               "dmabuf IPC; HSA_ENABLE_IPC_MODE_LEGACY=0 is required): " + "; ".join(bad))
         # 4) slices (identical on every rank; 8-element = 16-B aligned boundaries)
         self.ranges = list(ranges)
         self.slices = []

@@ -279,6 +279,8 @@ def train(args):
     stopped_for_time = False
     stop_flag = torch.zeros(1, dtype=torch.int32, device=device)
     log_rank0("Starting training!")
+    if world_size > 1:
+        print(f"[Rank {rank}] Starting training on {device}", flush=True)
     loss = None
     while train_step < args.training_steps:
         train_step += 1

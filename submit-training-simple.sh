@@ -102,9 +102,17 @@ if [ "$PROFILE" -eq 1 ]; then
        "${CMD[@]}" --profile)
 fi
 echo "Running: ${CMD[*]}"
-# one task per GPU; SLURM_PROCID/SLURM_LOCALID select rank and device. srun runs in the
-# background so the trap below can forward SIGUSR1/SIGTERM while the shell waits.
-srun --kill-on-bad-exit=1 --gpus-per-task=1 --gpu-bind=closest "${CMD[@]}" &
+# one task per GPU; SLURM_PROCID selects the rank. By default every node GPU is visible to every
+# task (reference dist_utils.py:47,55) and SLURM_LOCALID selects the device; this is what peer IPC
+# (--allreduce xgmi) needs. PYRECOVER_GPU_BIND=closest isolates one GPU per task instead
+# (--gpus-per-task=1 --gpu-bind=closest): each task then sees device 0 and uses it
+# (pyrecover_amd/parallel/dist.py gpu_index). srun runs in the background so the trap below can
+# forward SIGUSR1/SIGTERM while the shell waits.
+SRUN_OPTS=(--kill-on-bad-exit=1)
+if [ -n "${PYRECOVER_GPU_BIND:-}" ]; then
+  SRUN_OPTS+=(--gpus-per-task=1 "--gpu-bind=${PYRECOVER_GPU_BIND}")
+fi
+srun "${SRUN_OPTS[@]}" "${CMD[@]}" &
 SRUN_PID=$!
 forward() {
   echo "batch shell: received $1, forwarding to the job step (srun pid $SRUN_PID)"

@@ -115,3 +115,56 @@ def test_usr1_to_batch_shell_writes_final_checkpoint_and_requeues_once(tmp_path)
     finals2 = sorted((ck / "slurmtest").glob("ckpt_*_final.pt"), key=lambda f: int(f.name.split("_")[1]))
     assert int(finals2[-1].name.split("_")[1]) > step
     assert (tmp_path / "slurm_calls.log").read_text().splitlines() == ["requeue 4242", "requeue 4242"]
+
+
+FAKE_SRUN_MULTI = """#!/bin/bash
+# fake srun for SLURM_NTASKS tasks on one node: task i gets SLURM_PROCID = SLURM_LOCALID = i
+while [[ "$1" == --* ]]; do shift; done
+PIDS=()
+for ((i = 0; i < ${SLURM_NTASKS:-1}; i++)); do
+  SLURM_PROCID=$i SLURM_LOCALID=$i "$@" &
+  PIDS+=($!)
+done
+trap 'kill -USR1 ${PIDS[@]}' USR1
+trap 'kill -TERM ${PIDS[@]}' TERM
+RC=0
+for p in "${PIDS[@]}"; do
+  while true; do wait $p; R=$?; kill -0 $p 2>/dev/null || break; done
+  [ $R -ne 0 ] && RC=$R
+done
+exit $RC
+"""
+
+
+def test_two_task_slurm_launch_binds_and_trains(tmp_path):
+    """The script's own multi-task path: 2 tasks (gloo on CPU), each reaches the training loop."""
+    b = _fake_bin(tmp_path)
+    (b / "srun").write_text(FAKE_SRUN_MULTI)
+    env = _env(tmp_path, 0)
+    env.update(SLURM_NTASKS="2", SLURM_NTASKS_PER_NODE="2", MASTER_PORT="29981")
+    args = ["--distributed", "--model-preset=llama-micro", "--synthetic-data", "--batch-size=4",
+            "--sequence-length=32", "--training-steps=3", "--exp_name=slurm2", f"--checkpoint-dir={tmp_path / 'ck'}"]
+    r = subprocess.run(["bash", str(ROOT / "submit-training-simple.sh")] + args, cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    txt = r.stdout + r.stderr
+    assert r.returncode == 0, txt[-4000:]
+    for rank in (0, 1):
+        assert f"[Rank {rank}] world_size=2, local_rank={rank}, device=cpu" in txt, txt[-4000:]
+        assert f"[Rank {rank}] Starting training" in txt, txt[-4000:]
+    assert "Starting training!" in txt
+
+
+@pytest.mark.parametrize("count,lrank,want", [(1, 3, 0), (8, 3, 3), (4, 5, 1), (0, 2, 2)])
+def test_gpu_index_maps_to_a_visible_device(monkeypatch, count, lrank, want):
+    """SLURM per-task isolation shows ONE device (index 0) whatever SLURM_LOCALID is."""
+    import torch
+
+    from pyrecover_amd.parallel import dist as D
+
+    monkeypatch.delenv("PYRECOVER_LOCAL_DEVICE", raising=False)
+    monkeypatch.setenv("SLURM_LOCALID", str(lrank))
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: count > 0)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: count)
+    assert D.gpu_index(lrank) == want
+    monkeypatch.setenv("PYRECOVER_LOCAL_DEVICE", "0")
+    assert D.gpu_index(lrank) == 0
