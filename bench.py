@@ -47,6 +47,8 @@ def parse():
                     help="capture the step into a HIP graph after the warmup steps (train.py --compile)")
     ap.add_argument("--phase-timing", action="store_true",
                     help="record device events around forward / backward / optimizer of each timed step")
+    ap.add_argument("--no-comm-timing", action="store_true",
+                    help="W > 1: skip the per-bucket collective timing (events; no host sync in the step)")
     ap.add_argument("--cpu", action="store_true",
                     help="run on the CPU over gloo (tests of the launcher and the DDP path; not a benchmark)")
     ap.add_argument("--gemm-tuning", choices=["auto", "off", "tune"], default="auto",
@@ -91,7 +93,7 @@ def main():
     from pyrecover_amd.optim.adamw import FlatAdamW
     from pyrecover_amd.optim.lr import build_lr_scheduler
     from pyrecover_amd.parallel import dist as D
-    from pyrecover_amd.parallel.ddp import GradReducer, broadcast_flat
+    from pyrecover_amd.parallel.ddp import GradReducer, broadcast_flat, comm_env
     from pyrecover_amd.utils.flops import num_flop_per_token
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
@@ -126,6 +128,7 @@ def main():
     if world > 1:
         broadcast_flat(flat)
     reducer = GradReducer(flat, bucket_cap_mb=args.bucket_mb, backend=args.allreduce)
+    timer = reducer.enable_comm_timing() if world > 1 and not args.no_comm_timing else None
     opt = FlatAdamW(flat, lr=args.lr, fused=True, grad_scale=1.0 / world)
     if not args.no_overlap_optimizer:
         opt.enable_overlap(reducer)
@@ -159,7 +162,10 @@ def main():
             sched.step()
             return loss
         n_eager[0] += 1
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if timed and dev.type == "cuda" else None
+        if timed and timer is not None:
+            timer.begin_step()
+        ev = ([torch.cuda.Event(enable_timing=True) for _ in range(4)]
+              if timed and args.phase_timing and dev.type == "cuda" else None)
         opt.zero_grad()
         if ev:
             ev[0].record()
@@ -187,7 +193,7 @@ def main():
     for i in range(args.steps):
         if args.profile_steps and i < args.profile_steps and dev.type == "cuda":
             torch.cuda.nvtx.range_push(f"step{i}")
-        loss = step(timed=args.phase_timing)
+        loss = step(timed=True)
         if args.profile_steps and i < args.profile_steps and dev.type == "cuda":
             torch.cuda.nvtx.range_pop()
     sync()
@@ -204,6 +210,13 @@ def main():
     tps = tokens / dt
     n_params = model.num_params()
     fpt = num_flop_per_token(model.num_params(exclude_embedding=True), cfg)
+    comm = None
+    if timer is not None:
+        comm = timer.summary(world)
+        e = torch.tensor([comm.get("exposed_comm_ms", 0.0)], device=dev, dtype=torch.float64)
+        per_rank = [torch.zeros_like(e) for _ in range(world)]
+        torch.distributed.all_gather(per_rank, e)
+        comm["exposed_comm_ms_per_rank"] = [round(float(x.item()), 3) for x in per_rank]
     if rank == 0:
         out = {
             "metric": f"tokens/sec at seq={S} bf16 (job aggregate over all GPUs; per-GPU in tokens_per_sec_per_gpu)",
@@ -238,6 +251,9 @@ def main():
             "gemm_table": bool(torch.cuda.tunable.is_enabled()) if dev.type == "cuda" else False,
             "hip_graph": bool(args.graph),
         }
+        if world > 1:
+            out["comm"] = comm
+            out["comm_env"] = comm_env()
         if phases:
             n = len(phases)
             out["phase_ms"] = {k: round(sum(e[i].elapsed_time(e[i + 1]) for e in phases) / n, 2)

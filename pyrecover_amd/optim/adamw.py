@@ -199,7 +199,10 @@ class FlatAdamW(torch.optim.AdamW):
         f = self.flat
         hi = f.numel if hi is None else hi
         gs = self.grad_scale * (float(self.grad_scale_dev[0]) if self.grad_scale_dev is not None else 1.0)
-        pd, gd, md, vd = f.data[lo:hi], f.grad[lo:hi], self.exp_avg[lo:hi], self.exp_avg_sq[lo:hi]
+        # `.data`: the update must not bump the flat buffer's autograd version counter (shared by
+        # every parameter view), or an overlapped bucket update during backward would invalidate
+        # weights other layers saved for their backward (the HIP kernels write through pointers)
+        pd, gd, md, vd = f.data.data[lo:hi], f.grad[lo:hi], self.exp_avg[lo:hi], self.exp_avg_sq[lo:hi]
         ct = torch.promote_types(pd.dtype, torch.float32)  # fp32 opmath; fp64 models stay fp64
         p = pd.to(ct)
         gr = gd.to(ct) * gs

@@ -27,3 +27,10 @@ def test_bench_gpus2_spawns_two_ranks(cuda):
     assert out["n_gpus"] == 2 and out["ranks_seen"] == 2, out
     assert out["config"]["parallelism"] == "dp2"
     assert out["value"] > 0 and out["final_loss"] == out["final_loss"]
+    # N-GPU diagnostics recorded with HIP events
+    c = out["comm"]
+    assert c["timing_source"] == "hip events" and len(c["exposed_comm_ms_per_rank"]) == 2
+    assert c["exposed_comm_ms"] >= 0 and c["allreduce_busy_ms"] > 0
+    assert len(c["buckets"]) == out["config"]["grad_buckets"]
+    assert all(b["ms"] >= 0 and b["mib"] > 0 for b in c["buckets"])
+    assert "comm_env" in out

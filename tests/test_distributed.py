@@ -148,6 +148,12 @@ def test_bench_self_spawns_ranks():
     assert out["n_gpus"] == 2 and out["ranks_seen"] == 2, out
     assert out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 4
     assert out["config"]["dist_backend"] == "gloo"
+    # N-GPU diagnostics (exposed communication, per-bucket all-reduce time/bandwidth, RCCL env)
+    c = out["comm"]
+    assert c["exposed_comm_ms"] >= 0 and len(c["exposed_comm_ms_per_rank"]) == 2
+    assert len(c["buckets"]) == out["config"]["grad_buckets"] and c["allreduce_busy_ms"] > 0
+    assert all(b["ms"] >= 0 and b["mib"] > 0 for b in c["buckets"])
+    assert isinstance(out["comm_env"], dict)
 
 
 def test_bench_rejects_world_mismatch():
@@ -205,3 +211,21 @@ def test_xgmi_host_sequence_words(tmp_path):
     for r in range(2):
         name, exists = open(tmp_path / f"hs_{r}.txt").read().split()
         assert name.startswith("pra_xgmi_") and exists == "False"
+
+
+def test_bench_cpu_overlapped_optimizer_many_buckets():
+    """Overlapped AdamW updates bucket by bucket DURING backward; on the CPU path this must not
+    bump the flat buffer's autograd version counter (it invalidated saved weights of layers whose
+    backward had not run yet)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "2"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--cpu", "--model",
+                        "llama-micro", "--seq-len", "64", "--batch-per-gpu", "2", "--steps", "2", "--warmup", "1",
+                        "--bucket-mb", "0.02"], capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _bench_json(r.stdout)
+    assert out["config"]["grad_buckets"] > 3 and len(out["comm"]["buckets"]) == out["config"]["grad_buckets"]
