@@ -72,10 +72,52 @@ def restore_rng_state(st: Dict[str, Any]):
         states = st["torch_cuda"]
         if len(states) == torch.cuda.device_count():
             torch.cuda.set_rng_state_all(states)
+    if "torch_cuda_device" in st and torch.cuda.is_available():
+        torch.cuda.set_rng_state(st["torch_cuda_device"])  # this rank's own device
+
+
+def capture_rank_rng_state() -> Dict[str, Any]:
+    """This rank's RNG streams: CPU, python and the generator of the rank's own device."""
+    st = {"torch_cpu": torch.get_rng_state(), "python": random.getstate()}
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        st["torch_cuda_device"] = torch.cuda.get_rng_state()
+    return st
+
+
+def gather_rng_states() -> Optional[List[Dict[str, Any]]]:
+    """Collective: every rank's :func:`capture_rank_rng_state`, indexed by rank (None without a
+    multi-rank process group). Checkpoints store the list as ``pyrecover_state.rng_per_rank`` so
+    a resumed DDP job restores each rank's own streams, not rank 0's."""
+    if not (torch.distributed.is_available() and torch.distributed.is_initialized()):
+        return None
+    w = torch.distributed.get_world_size()
+    if w <= 1:
+        return None
+    out: List[Any] = [None] * w
+    torch.distributed.all_gather_object(out, capture_rank_rng_state())
+    return out
+
+
+def restore_rng_from(ps: Optional[Dict[str, Any]]):
+    """Restore this rank's RNG from a checkpoint's ``pyrecover_state``: its own entry of
+    ``rng_per_rank`` when the world size matches, else the saving process's ``rng``."""
+    ps = ps or {}
+    per = ps.get("rng_per_rank")
+    if per:
+        per = [per[k] for k in sorted(per, key=int)] if isinstance(per, dict) else list(per)
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        rank, world = torch.distributed.get_rank(), torch.distributed.get_world_size()
+    else:
+        rank, world = 0, 1
+    if per and len(per) == world:
+        restore_rng_state(per[rank])
+    else:
+        restore_rng_state(ps.get("rng"))
 
 
 def build_state(model, optimizer, lr_scheduler=None, sampler=None, step: int = 0, epoch: Optional[int] = None,
-                extra: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
+                extra: Optional[Dict[str, Any]] = None,
+                rng_per_rank: Optional[List[Dict[str, Any]]] = None) -> Dict[str, Any]:
     """The reference's vanilla checkpoint dict (reference pyrecover/checkpoint.py:60-73) plus a
     ``pyrecover_state`` entry (RNG, sampler cursor, run metadata) that reference loaders ignore."""
     m = unwrap(model)
@@ -92,6 +134,8 @@ def build_state(model, optimizer, lr_scheduler=None, sampler=None, step: int = 0
     ps = {"format": "pyrecover_amd/1", "rng": capture_rng_state(), "saved_at": time.time()}
     if torch.distributed.is_available() and torch.distributed.is_initialized():
         ps["world_size"] = torch.distributed.get_world_size()
+    if rng_per_rank is not None:
+        ps["rng_per_rank"] = rng_per_rank
     if extra:
         ps.update(extra)
     state["pyrecover_state"] = ps

@@ -313,7 +313,7 @@ def finish_state(model, optimizer, lr_scheduler, sampler, ckpt, plan: Plan) -> T
         lr_scheduler.load_state_dict(sd)
     if sampler is not None and "sampler_state" in ckpt and hasattr(sampler, "load_state_dict"):
         sampler.load_state_dict(ckpt["sampler_state"])
-    core.restore_rng_state((ckpt.get("pyrecover_state") or {}).get("rng"))
+    core.restore_rng_from(ckpt.get("pyrecover_state"))
     return ckpt.get("epoch", 0), ckpt.get("step", 0)
 
 

@@ -99,7 +99,8 @@ def save_ckpt_distributed(model, optimizer, lr_scheduler=None, sampler=None, ste
         dist.barrier()
     core.wait_all()
     finalize_pending()
-    state = core.build_state(model, optimizer, lr_scheduler, sampler, step, epoch, extra_state)
+    rngs = core.gather_rng_states() if is_distributed else None  # collective: every rank's streams
+    state = core.build_state(model, optimizer, lr_scheduler, sampler, step, epoch, extra_state, rngs)
     # dcp key layout: "metadata" holds epoch/step (reference checkpoint.py:254-258)
     dstate: Dict[str, Any] = {"model": state["model"], "optimizer": state["optimizer"],
                               "metadata": {"epoch": epoch, "step": step}}
@@ -109,6 +110,8 @@ def save_ckpt_distributed(model, optimizer, lr_scheduler=None, sampler=None, ste
         dstate["sampler"] = state["sampler_state"]
     dstate["pyrecover_state"] = {"rng": state["pyrecover_state"]["rng"],
                                  "format": state["pyrecover_state"]["format"]}
+    if rngs is not None:
+        dstate["pyrecover_state"]["rng_per_rank"] = {str(r): st for r, st in enumerate(rngs)}
     items = flatten_state(dstate)
     owners = assign_owners(items, world)
     mine = {k: v for k, v in items.items() if owners[k] == rank}

@@ -43,8 +43,9 @@ def save_ckpt_vanilla(model, optimizer, lr_scheduler=None, sampler=None, step: i
                       extra_state=None) -> str:
     if is_distributed:
         dist.barrier()
+    rngs = core.gather_rng_states() if is_distributed else None  # collective: every rank's streams
     if rank == 0 or not is_distributed:
-        state = core.build_state(model, optimizer, lr_scheduler, sampler, step, epoch, extra_state)
+        state = core.build_state(model, optimizer, lr_scheduler, sampler, step, epoch, extra_state, rngs)
         ck = core.Checkpointer.get(_device_of(model))
         staged = ck.stage(state)
         prefix = Path(checkpoint_path).name
@@ -101,8 +102,7 @@ def load_state_into(model, optimizer, lr_scheduler, sampler, ckpt) -> Tuple[int,
         lr_scheduler.load_state_dict(sd)
     if sampler is not None and "sampler_state" in ckpt and hasattr(sampler, "load_state_dict"):
         sampler.load_state_dict(ckpt["sampler_state"])
-    ps = ckpt.get("pyrecover_state") or {}
-    core.restore_rng_state(ps.get("rng"))
+    core.restore_rng_from(ckpt.get("pyrecover_state"))
     return ckpt.get("epoch", 0), ckpt.get("step", 0)
 
 

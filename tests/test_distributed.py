@@ -229,3 +229,48 @@ def test_bench_cpu_overlapped_optimizer_many_buckets():
     assert r.returncode == 0, r.stderr[-3000:]
     out = _bench_json(r.stdout)
     assert out["config"]["grad_buckets"] > 3 and len(out["comm"]["buckets"]) == out["config"]["grad_buckets"]
+
+
+def _rng_worker(rank, world, port, out_dir, fmt):
+    import random
+
+    import torch.distributed as dist
+
+    from pyrecover_amd.ckpt import sharded, vanilla
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    torch.manual_seed(0)
+    model = torch.nn.Linear(8, 8)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+    model(torch.randn(2, 8)).sum().backward()
+    opt.step()
+    torch.manual_seed(100 + rank)  # every rank its own streams
+    random.seed(7 * rank + 1)
+    path = os.path.join(out_dir, "ckpt_1.pt" if fmt == "vanilla" else "ckpt_1")
+    save = vanilla.save_ckpt_vanilla if fmt == "vanilla" else sharded.save_ckpt_distributed
+    load = vanilla.load_ckpt_vanilla if fmt == "vanilla" else sharded.load_ckpt_distributed
+    save(model, opt, step=1, epoch=1, checkpoint_path=path, verify=False, is_distributed=True, rank=rank)
+    want = (torch.rand(4), random.random())
+    torch.manual_seed(999)
+    random.seed(999)
+    load(model, opt, checkpoint_path=path, experiment_dir=out_dir, verify=False, is_distributed=True, rank=rank)
+    got = (torch.rand(4), random.random())
+    torch.save({"want": want, "got": got}, os.path.join(out_dir, f"rng_{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fmt", ["vanilla", "sharded"])
+def test_checkpoint_restores_each_ranks_own_rng(tmp_path, fmt):
+    """Every rank's RNG streams are saved (pyrecover_state.rng_per_rank) and each rank restores its
+    own, not the saving rank's (reference saves none)."""
+    mp.spawn(_rng_worker, args=(2, _free_port(), str(tmp_path), fmt), nprocs=2, join=True)
+    r = [torch.load(tmp_path / f"rng_{i}.pt", weights_only=False) for i in range(2)]
+    for x in r:
+        assert torch.equal(x["want"][0], x["got"][0]) and x["want"][1] == x["got"][1]
+    assert not torch.equal(r[0]["got"][0], r[1]["got"][0])
+    if fmt == "vanilla":  # the reference key set is untouched; the extra entry rides along
+        ck = torch.load(tmp_path / "ckpt_1.pt", weights_only=False)
+        assert {"epoch", "step", "model", "optimizer"} <= set(ck)
+        assert len(ck["pyrecover_state"]["rng_per_rank"]) == 2
