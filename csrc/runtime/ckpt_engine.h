@@ -83,6 +83,18 @@ class Md5Pipe {
     enqueue({buf->data(), n, buf});
   }
   void push_borrowed(const void* p, size_t n) { enqueue({(const uint8_t*)p, n, nullptr}); }
+  // drop everything still queued and stop (the digest is then meaningless)
+  void abort() {
+    if (!th_.joinable()) return;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      q_.clear();
+      done_ = true;
+    }
+    cv_.notify_all();
+    cv_space_.notify_all();
+    th_.join();
+  }
   std::string finish() {
     if (th_.joinable()) {
       {
@@ -283,12 +295,17 @@ struct JobResult {
 };
 
 // Streaming MD5 of an open file from its start (double-buffered reads on this thread, hashing
-// on the Md5Pipe thread).
-inline std::string md5_fd(int fd) {
+// on the Md5Pipe thread). `cancel` (optional) is checked between reads: once set, the digest is
+// dropped and md5_fd throws.
+inline std::string md5_fd(int fd, const std::atomic<bool>* cancel = nullptr) {
   Md5Pipe md5;
   constexpr size_t kBuf = 32u << 20;
   uint64_t pos = 0;
   for (;;) {
+    if (cancel != nullptr && cancel->load(std::memory_order_relaxed)) {
+      md5.abort();
+      throw std::runtime_error("md5: cancelled");
+    }
     auto buf = std::make_shared<std::vector<uint8_t>>(kBuf);
     ssize_t n;
     do {
@@ -468,13 +485,21 @@ class CkptEngine {
     e.swap(md5st_->error);
     return e;
   }
-  // Stop waiting for deferred digests (a job about to be killed by its wall-clock limit): they
-  // keep running until the process exits; a digest cut short leaves no `.md5` (the `.md5parts`
-  // written with the archive still verify it).
+  // Cancel deferred digests (a job about to be killed by its wall-clock limit): each stops at its
+  // next 32 MiB read and is joined here, so no digest thread outlives the call (interpreter
+  // shutdown, static destructors). A cancelled digest leaves no `.md5`; the `.md5parts` written
+  // with the archive still verify it.
   void abandon_md5() {
-    std::lock_guard<std::mutex> g(md5_th_mu_);
-    for (auto& t : md5_th_) t.detach();
-    md5_th_.clear();
+    md5st_->cancel = true;
+    std::vector<std::thread> th;
+    {
+      std::lock_guard<std::mutex> g(md5_th_mu_);
+      th.swap(md5_th_);
+    }
+    for (auto& t : th) t.join();
+    std::lock_guard<std::mutex> g(md5st_->mu);
+    md5st_->error.clear();  // "cancelled" is not a failure
+    md5st_->cancel = false;  // later saves digest again
   }
   bool md5_pending() {
     std::lock_guard<std::mutex> g(md5st_->mu);
@@ -647,17 +672,23 @@ class CkptEngine {
     own(std::move(c));
   }
 
-  static void pwrite_all(int fd, const uint8_t* b, size_t n, uint64_t pos) {
+  // 0, or the errno of the first failed pwrite
+  static int try_pwrite_all(int fd, const uint8_t* b, size_t n, uint64_t pos) {
     while (n) {
       const ssize_t w = ::pwrite(fd, b, std::min<size_t>(n, 1u << 30), (off_t)pos);
       if (w < 0) {
         if (errno == EINTR) continue;
-        throw std::runtime_error(std::string("ckpt_engine: write failed: ") + strerror(errno));
+        return errno;
       }
       b += w;
       pos += (uint64_t)w;
       n -= (size_t)w;
     }
+    return 0;
+  }
+  static void pwrite_all(int fd, const uint8_t* b, size_t n, uint64_t pos) {
+    if (const int e = try_pwrite_all(fd, b, n, pos))
+      throw std::runtime_error(std::string("ckpt_engine: write failed: ") + strerror(e));
   }
 
   // The file is written segment by segment (kSegBytes) by kWriters threads, each hashing the
@@ -771,7 +802,17 @@ class CkptEngine {
     // buffers and DMA'd to the device, skipping the page-cache copy and most of the fsync flush
     const char* dw = std::getenv("PYRECOVER_CKPT_DIRECT_WRITE");
     int dfd = (dw != nullptr && dw[0] == '0') ? -1 : ::open(tmp.c_str(), O_WRONLY | O_CLOEXEC | O_DIRECT);
+    // Some filesystems (FUSE, overlay, network) accept the O_DIRECT open but refuse the aligned
+    // pwrite with EINVAL: the first such refusal switches this and every later chunk of the save to
+    // buffered writes on `fd` (as Reader::read_impl does for reads). PYRECOVER_FAULT_DIRECT_EINVAL=1
+    // injects that refusal on the first direct write (tests).
     r.direct = dfd >= 0;
+    std::atomic<bool> use_direct{dfd >= 0};
+    static const bool inject_einval = [] {
+      const char* e = std::getenv("PYRECOVER_FAULT_DIRECT_EINVAL");
+      return e != nullptr && e[0] == '1';
+    }();
+    std::atomic<bool> injected{false};
     constexpr uint64_t kBounce = 64ull << 20;
     std::vector<std::thread> ws;
     for (int t = 0; t < nthreads; ++t) {
@@ -798,9 +839,15 @@ class CkptEngine {
               }
               if (bounce) {
                 if (want_md5) EVP_DigestUpdate(ctx, bounce, e - c);
-                const uint64_t len = (e - c + 4095) & ~uint64_t(4095);  // tail padded; truncated below
-                std::memset(bounce + (e - c), 0, len - (e - c));
-                pwrite_all(dfd, bounce, len, c);
+                int rc = EINVAL;
+                if (use_direct.load()) {
+                  const uint64_t len = (e - c + 4095) & ~uint64_t(4095);  // tail padded; truncated below
+                  std::memset(bounce + (e - c), 0, len - (e - c));
+                  rc = (inject_einval && !injected.exchange(true)) ? EINVAL : try_pwrite_all(dfd, bounce, len, c);
+                  if (rc == EINVAL) use_direct = false;
+                  else if (rc != 0) throw std::runtime_error(std::string("ckpt_engine: write failed: ") + strerror(rc));
+                }
+                if (rc == EINVAL) pwrite_all(fd, bounce, e - c, c);  // buffered, exact length
               }
             }
             if (want_md5) r.seg_md5[s] = digest_hex(ctx);
@@ -818,6 +865,7 @@ class CkptEngine {
       ::close(dfd);
       if (err.empty() && total % 4096 && ::ftruncate(fd, (off_t)total) != 0) err = "ckpt_engine: ftruncate failed";
     }
+    r.direct = r.direct && use_direct.load();
     r.write_seconds = std::chrono::duration<double>(clk::now() - t_write).count();
     const auto t_sync = clk::now();
     if (err.empty() && do_fsync && ::fsync(fd) != 0) err = "ckpt_engine: fsync failed";
@@ -853,17 +901,26 @@ class CkptEngine {
       try {
         const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
         if (fd < 0) throw std::runtime_error("ckpt_engine: deferred md5: cannot open " + path);
+        struct stat before {};
         std::string md5;
         try {
-          md5 = md5_fd(fd);
+          if (::fstat(fd, &before) != 0) throw std::runtime_error("ckpt_engine: deferred md5: fstat failed");
+          md5 = md5_fd(fd, &st->cancel);
         } catch (...) {
           ::close(fd);
           throw;
         }
         ::close(fd);
-        write_sidecar(path + ".md5", md5, do_fsync);
+        // write the sidecar only if `path` is still the file that was hashed: retention may have
+        // deleted it meanwhile (no orphan `.md5`), or a new save of the same path may have
+        // replaced it (its own digest owns the sidecar; no false mismatch on resume)
+        struct stat now {};
+        if (::stat(path.c_str(), &now) == 0 && now.st_ino == before.st_ino && now.st_dev == before.st_dev &&
+            now.st_mtim.tv_sec == before.st_mtim.tv_sec && now.st_mtim.tv_nsec == before.st_mtim.tv_nsec &&
+            now.st_size == before.st_size)
+          write_sidecar(path + ".md5", md5, do_fsync);
       } catch (const std::exception& e) {
-        err = e.what();
+        if (!st->cancel.load()) err = e.what();
       }
       std::lock_guard<std::mutex> g2(st->mu);
       if (!err.empty()) st->error = err;
@@ -893,6 +950,7 @@ class CkptEngine {
     std::mutex mu;
     int running = 0;
     std::string error;
+    std::atomic<bool> cancel{false};
   };
   std::vector<std::thread> md5_th_;  // deferred whole-file digests
   std::mutex md5_th_mu_;

@@ -238,21 +238,26 @@ def execute(plan: Plan, buffers: Sequence[torch.Tensor], verify: bool = False, m
     files = dict(plan.files)
     if verify and md5parts is not None and whole_md5_path is not None:
         files.setdefault(whole_md5_path, [])  # segments are hashed even if nothing lands natively
-    for path, items in files.items():
-        native = _partition(items, buffers, rank, world)
-        stats["item_bytes"] += sum(n for _, n, _ in native)
-        hash_segs = []
-        if verify and md5parts is not None and path == whole_md5_path:
-            hash_segs = [s for s in range(len(md5parts[2])) if s % world == rank]
-            stats["verified"] = "md5parts"
-        res = _reader(dev_index).read(path, native, hash_segs, READ_THREADS, DIRECT_IO)
-        if not res["ok"]:
-            raise RuntimeError(f"checkpoint read of {path} failed: {res['error']}")
-        stats["bytes_read"] += res["bytes_read"]
-        stats["direct"] = res["direct"]
-        for s in hash_segs:
-            if res["seg_md5"][s] != md5parts[2][s]:
-                bad.append(s)
+    try:
+        for path, items in files.items():
+            native = _partition(items, buffers, rank, world)
+            stats["item_bytes"] += sum(n for _, n, _ in native)
+            hash_segs = []
+            if verify and md5parts is not None and path == whole_md5_path:
+                hash_segs = [s for s in range(len(md5parts[2])) if s % world == rank]
+                stats["verified"] = "md5parts"
+            res = _reader(dev_index).read(path, native, hash_segs, READ_THREADS, DIRECT_IO)
+            if not res["ok"]:
+                raise RuntimeError(f"checkpoint read of {path} failed: {res['error']}")
+            stats["bytes_read"] += res["bytes_read"]
+            stats["direct"] = res["direct"]
+            for s in hash_segs:
+                if res["seg_md5"][s] != md5parts[2][s]:
+                    bad.append(s)
+    finally:
+        # resume happens once per job: free the reader's pinned buffers (READ_THREADS x 2 x 64 MiB)
+        # instead of holding them for the rest of training
+        _readers.pop(dev_index, None)
     stats["read_s"] = time.perf_counter() - t0
     if is_distributed:
         flag = torch.tensor([len(bad)], dtype=torch.int64, device=dev if dev.type == "cuda" else "cpu")

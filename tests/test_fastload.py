@@ -178,3 +178,46 @@ def test_two_ranks_read_half_and_allgather(tmp_path, kind):
         assert torch.equal(got["v"], opt.exp_avg_sq) and got["step"] == opt._step
         # each rank places its half of every flat buffer (plus a < world-byte tail) from the file
         assert total // 2 <= got["item_bytes"] <= total // 2 + 3 * 2
+
+
+_EINVAL_SCRIPT = r"""
+import json, sys, torch
+sys.path.insert(0, {root!r})
+from pyrecover_amd.ckpt import core
+from pyrecover_amd.ckpt.vanilla import save_ckpt_vanilla, load_ckpt_vanilla
+from pyrecover_amd.config import get_preset
+from pyrecover_amd.models.llama import Transformer
+from pyrecover_amd.optim.adamw import FlatAdamW
+torch.manual_seed(0)
+m = Transformer(get_preset("llama-micro", seq_len=64)); flat = m.flatten_(); opt = FlatAdamW(flat, lr=1e-3)
+save_ckpt_vanilla(m, opt, step=3, epoch=1, checkpoint_path={path!r}, verify=True)
+direct = core.WRITE_STATS["last"]["direct"]
+ref = torch.load({path!r}, weights_only=True)
+m2 = Transformer(get_preset("llama-micro", seq_len=64)); flat2 = m2.flatten_(); opt2 = FlatAdamW(flat2, lr=1e-3)
+load_ckpt_vanilla(m2, opt2, checkpoint_path={path!r}, verify=True)
+ok = torch.equal(flat.data, flat2.data) and all(torch.equal(ref["model"][k], v) for k, v in m.state_dict().items())
+print(json.dumps({{"direct": direct, "ok": ok}}))
+"""
+
+
+@pytest.mark.parametrize("inject", [False, True])
+def test_direct_write_refused_falls_back_to_buffered(tmp_path, inject):
+    """A filesystem that accepts the O_DIRECT open but refuses the aligned pwrite (EINVAL) must not
+    fail the save: the writer switches to buffered writes (PYRECOVER_FAULT_DIRECT_EINVAL injects
+    the refusal on the first direct write)."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path = str(tmp_path / "ckpt_3.pt")
+    env = dict(os.environ, PYRECOVER_FAULT_DIRECT_EINVAL="1" if inject else "0", OMP_NUM_THREADS="2")
+    r = subprocess.run([sys.executable, "-c", _EINVAL_SCRIPT.format(root=root, path=path)], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["ok"]
+    with open(path, "rb") as f:
+        assert hashlib.md5(f.read()).hexdigest() == open(path + ".md5").read()
+    if inject:
+        assert out["direct"] is False
