@@ -469,6 +469,18 @@ at::Tensor transpose2d(const at::Tensor& src, c10::optional<at::Tensor> out) {
   return dst;
 }
 
+// CU count of a tensor's device (cached per device)
+int device_cus(const at::Tensor& t) {
+  static int cached[64] = {0};
+  const int d = t.device().index();
+  if (d >= 0 && d < 64 && cached[d] > 0) return cached[d];
+  int cus = 0;
+  TORCH_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && cus > 0,
+              "pyrecover_amd: device attribute");
+  if (d >= 0 && d < 64) cached[d] = cus;
+  return cus;
+}
+
 // out [M, N] (+)= a^T b with a [K, M], b [K, N] (both row-major, K = tokens): the weight gradient
 // dW = dY^T X straight from the activations (no transposed copies), hand-written MFMA kernel.
 void wgrad_mm_(const at::Tensor& a, const at::Tensor& b, at::Tensor out, bool accumulate) {
@@ -486,21 +498,90 @@ void wgrad_mm_(const at::Tensor& a, const at::Tensor& b, at::Tensor out, bool ac
   TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 32 == 0 && K > 0, "wgrad_mm: M, N % 256 and K % 32");
   TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && out.stride(0) % 8 == 0, "wgrad_mm: 16-B rows");
   const c10::DeviceGuard guard(a.device());
-  // scratch of the split tail (fp32 partial tiles + tickets), from the caching allocator so it is
-  // graph-capture safe; only when the tiles do not fill whole rounds of the CUs
-  const int64_t nwg = (M / 256) * (N / 256);
-  int cus = 0;
-  TORCH_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, a.device().index()) == hipSuccess,
-              "wgrad_mm: device attribute");
+  // scratch of the split tail (fp32 partial tiles + tickets), sized exactly for the launcher's
+  // split choice, from the caching allocator (graph-capture safe); none when tiles fill whole rounds
+  const int cus = device_cus(a);
+  const long nws = pra_wgrad_ws_floats((int)M, (int)N, (int)K, cus);
   at::Tensor ws, tickets;
-  if (nwg > cus && nwg % cus != 0) {
-    ws = at::empty({(int64_t)pra_wgrad_ws_floats()}, a.options().dtype(at::kFloat));
-    tickets = at::empty({(int64_t)pra_wgrad_ticket_count()}, a.options().dtype(at::kInt));
+  if (nws > 0) {
+    ws = at::empty({(int64_t)nws}, a.options().dtype(at::kFloat));
+    tickets = at::empty({(int64_t)pra_wgrad_ticket_count((int)M, (int)N, (int)K, cus)}, a.options().dtype(at::kInt));
   }
   check(pra_wgrad_gemm(dt(a), a.data_ptr(), b.data_ptr(), out.data_ptr(), (int)M, (int)N, (int)K, a.stride(0),
                        b.stride(0), out.stride(0), accumulate ? 1 : 0, ws.defined() ? ws.data_ptr<float>() : nullptr,
-                       tickets.defined() ? tickets.data_ptr<int>() : nullptr, stream_of(a)),
+                       tickets.defined() ? tickets.data_ptr<int>() : nullptr, cus, stream_of(a)),
         "wgrad_mm");
+}
+
+// NT GEMM with a fused epilogue (gemm_nt.hip): a [M, K], b [N, K] row-major (K-contiguous).
+//   epi 0: out [M, N] = a b^T
+//   epi 1: SwiGLU forward, b = W1|W3 [2F, K]: out = gu [M, 2F], out2 = a [M, F]
+//   epi 2: SwiGLU backward, b [F, K] (W2^T): da = a b^T is consumed in the epilogue, which
+//          overwrites g, u in out = gu [M, 2F] with dg, du
+//   epi 3: RoPE on the first nrot columns of out [M, N] (tab float32 [S, D/2, 2])
+void gemm_nt_(const at::Tensor& a, const at::Tensor& b, at::Tensor out, int64_t epi,
+              const c10::optional<at::Tensor>& out2, const c10::optional<at::Tensor>& tab, int64_t S, int64_t D,
+              int64_t nrot) {
+  const Range range_("pyrecover::gemm_nt");
+  check_dev(a, "a");
+  check_row_major(a, "a");
+  check_row_major(b, "b");
+  check_row_major(out, "out");
+  same_dev(a, b, "b");
+  same_dev(a, out, "out");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K, "gemm_nt: a [M, K] and b [N, K]");
+  TORCH_CHECK(a.scalar_type() == b.scalar_type() && a.scalar_type() == out.scalar_type() && a.element_size() == 2,
+              "gemm_nt: bf16/fp16 operands of one dtype");
+  TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 32 == 0 && K > 0, "gemm_nt: M, N % 256 and K % 32");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && out.stride(0) % 8 == 0, "gemm_nt: 16-B rows");
+  TORCH_CHECK(epi >= 0 && epi <= 3, "gemm_nt: epi in 0..3");
+  int64_t F = 0;
+  void* c2 = nullptr;
+  int64_t ldc2 = 0;
+  const void* tabp = nullptr;
+  if (epi == 0 || epi == 3) {
+    TORCH_CHECK(out.size(0) == M && out.size(1) == N, "gemm_nt: out [M, N]");
+  }
+  if (epi == 1) {
+    F = N / 2;
+    TORCH_CHECK(N % 2 == 0 && F % 128 == 0, "gemm_nt swiglu: b = W1|W3 [2F, K], F % 128");
+    TORCH_CHECK(out.size(0) == M && out.size(1) == N, "gemm_nt swiglu: gu [M, 2F]");
+    TORCH_CHECK(out2.has_value(), "gemm_nt swiglu: needs out2 = a [M, F]");
+    check_row_major(*out2, "out2");
+    same_dev(a, *out2, "out2");
+    TORCH_CHECK(out2->scalar_type() == a.scalar_type() && out2->size(0) == M && out2->size(1) == F &&
+                    out2->stride(0) % 8 == 0,
+                "gemm_nt swiglu: a [M, F]");
+    c2 = out2->data_ptr();
+    ldc2 = out2->stride(0);
+  }
+  if (epi == 2) {
+    F = N;
+    TORCH_CHECK(out.size(0) == M && out.size(1) == 2 * F, "gemm_nt swiglu bwd: gu [M, 2F] with b [F, K]");
+  }
+  if (epi == 3) {
+    TORCH_CHECK(tab.has_value(), "gemm_nt rope: needs tab");
+    same_dev(a, *tab, "tab");
+    TORCH_CHECK(tab->scalar_type() == at::kFloat && tab->is_contiguous() && tab->numel() >= S * (D / 2) * 2,
+                "gemm_nt rope: tab float32 [>= S, D/2, 2]");
+    TORCH_CHECK(S > 0 && D > 0 && D % 8 == 0 && nrot % D == 0 && nrot <= N && M % S == 0,
+                "gemm_nt rope: S, D % 8, nrot % D, tokens % S");
+    tabp = tab->data_ptr();
+  }
+  const c10::DeviceGuard guard(a.device());
+  const int cus = device_cus(a);
+  const long nws = pra_gemm_nt_ws_floats((int)M, (int)N, (int)K, cus);
+  at::Tensor ws, tickets;
+  if (nws > 0) {  // split tail scratch: exactly R * S partial tiles, from the caching allocator (graph-safe)
+    ws = at::empty({(int64_t)nws}, a.options().dtype(at::kFloat));
+    tickets = at::empty({(int64_t)pra_gemm_nt_ticket_count((int)M, (int)N, (int)K, cus)}, a.options().dtype(at::kInt));
+  }
+  check(pra_gemm_nt(dt(a), (int)epi, a.data_ptr(), b.data_ptr(), out.data_ptr(), (int)M, (int)N, (int)K, a.stride(0),
+                    b.stride(0), out.stride(0), c2, ldc2, (int)F, tabp, (int)S, (int)D, (int)nrot,
+                    ws.defined() ? ws.data_ptr<float>() : nullptr, tickets.defined() ? tickets.data_ptr<int>() : nullptr,
+                    cus, stream_of(a)),
+        "gemm_nt");
 }
 
 // returns fp32 [2] = {norm, clip_coef}
@@ -666,6 +747,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("gscale"), py::arg("gscale_dev") = py::none(), py::arg("hyper_dev") = py::none());
   m.def("grad_norm", &grad_norm);
   m.def("wgrad_mm_", &wgrad_mm_);
+  m.def("gemm_nt_", &gemm_nt_, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("epi") = 0,
+        py::arg("out2") = py::none(), py::arg("tab") = py::none(), py::arg("S") = 0, py::arg("D") = 0,
+        py::arg("nrot") = 0);
   m.def("transpose2d", &transpose2d, py::arg("src"), py::arg("out") = py::none());
   m.def("swiglu_bwd_t_", &swiglu_bwd_t_);
   m.def("swiglu_fwd_t", &swiglu_fwd_t);

@@ -1,0 +1,391 @@
+// Forward / data-gradient GEMM for gfx950 (CDNA4) with fused epilogues:
+//
+//     C[M][N] = sum_k A[m][k] * B[n][k]        (Y = X W^T, dX = dY W with W^T shadows)
+//
+// Both operands are K-contiguous (row-major activations [tokens, in] and weights [out, in]), the
+// "NT" layout of every forward projection and of the data gradients (ops/fused.py keeps
+// transposed weight shadows so dX = dY W is NT too). Reference GEMM sites: model.py:171-177
+// (wq/wk/wv/wo), :264-269 (w1/w3/w2), :367 (output head).
+//
+// Machine (gemm_common.h): 256 x 256 tile, 4 waves of 128 x 128, 32-deep stages by LDS-DMA into a
+// 5-stage ring, counted vmcnt + raw s_barrier, v_mfma_f32_16x16x32, XCD-aware group-M order,
+// deterministic split-K tail. Operand tiles are [256 rows][32 k] (64-B rows) in LDS; MFMA operand
+// fragments (16 rows x 32 k) are ONE ds_read_b128 per lane: lane l reads row l & 15, k 8(l >> 4)..+7,
+// exactly the MFMA operand map. The 16-B chunks of each row are XOR-swizzled by g((row >> 2) & 3),
+// g = {0, 2, 3, 1}, which makes every ds_read_b128 lane group cover the 16 slots of a bank row once
+// (conflict-free); the LDS-DMA writes linearly and the swizzle is applied to its global source
+// address instead.
+//
+// Orientation: acc = mfma(B fragment, A fragment), so a lane holds one output row m and 4
+// consecutive columns n in its 4 registers: RoPE pairs (2i, 2i+1) are in one lane, and a lane
+// writes 8 contiguous bytes per 16 x 16 block.
+//
+// Epilogues (EPI):
+//   0 plain:        C = A B^T (bf16/fp16 rounding once)
+//   1 SwiGLU fwd:   B = W1|W3 [2F][K]; the B tile interleaves 128 gate rows with the matching
+//                   128 up rows so gate and up of a feature land in one lane; writes
+//                   gu = [g | u] (C, [M][2F]) and a = round(silu(g)) * u (C2, [M][F])
+//                   (the rounding points of swiglu_fwd_kernel, reference model.py:268-269)
+//   2 SwiGLU bwd:   C = da = dY W2 is never stored; the epilogue reads g, u from gu (C, in place)
+//                   and overwrites them with dg, du (swiglu_bwd_kernel's math)
+//   3 RoPE:         C = QKV with the interleaved-pair rotation (rope_kernel's math, reference
+//                   model.py:101-127) applied to the first `nrot` columns (q and k heads)
+// Requires M % 256 == 0, N % 256 == 0 (EPI 1: F % 128 == 0), K % 32 == 0, 16-B aligned rows.
+#include "gemm_common.h"
+
+#include <stdlib.h>
+
+namespace pra {
+namespace nt {
+
+using namespace gm;
+
+template <typename T>
+struct Epi {
+  T* c2;             // EPI 1: a [M][F]
+  long ldc2;
+  int F;             // EPI 1 / 2: gu holds g at [0, F) and u at [F, 2F)
+  const float2* tab; // EPI 3: (cos, sin) [S][D/2]
+  int S, D, nrot;    // EPI 3
+};
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
+__device__ __forceinline__ void rot_pair(float a, float b, float c, float s, float& o0, float& o1) {
+  o0 = __builtin_fmaf(a, c, -(b * s));
+  o1 = __builtin_fmaf(a, s, b * c);
+}
+template <typename T>
+__device__ __forceinline__ float rnd16(float v) {
+  return (float)(T)v;
+}
+template <typename T>
+__device__ __forceinline__ void unpack4(uint2 w, float (&o)[4]) {
+  const T* h = reinterpret_cast<const T*>(&w);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] = (float)h[e];
+}
+
+// the XOR swizzle of the 16-B chunk of row r: g((r >> 2) & 3), g = {0, 2, 3, 1}
+__device__ __forceinline__ int swz(int r) {
+  const int q = (r >> 2) & 3;
+  return (q >> 1) | (((q & 1) ^ (q >> 1)) << 1);
+}
+
+template <typename T, int EPI>
+__global__ __launch_bounds__(NTH) void gemm_nt_kernel(const T* __restrict__ A, const T* __restrict__ B,
+                                                      T* __restrict__ C, int M, int N, int K, long lda, long ldb,
+                                                      long ldc, Epi<T> ep, float* __restrict__ ws,
+                                                      int* __restrict__ tickets, int n_split, int S) {
+  __shared__ __attribute__((aligned(1024))) T smem[NS * 2 * TILE];
+  const int tiles_m = M / BM, tiles_n = N / BN, nwg = tiles_m * tiles_n, nk = K / BK;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  // DMA instruction i of wave w fills LDS bytes [(4i + w) KiB, +1 KiB) of an operand tile: rows
+  // 16 (4i + w) + lane / 4, swizzled chunk lane & 3 -> global chunk (lane & 3) ^ swz(row)
+  uint32_t offa[NI], offb[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int r = (i * 4 + wid) * 16 + (lane >> 2);
+    const int c = (lane & 3) ^ swz(r);
+    offa[i] = (uint32_t)((r * (int)lda + c * 8) * (int)sizeof(T));
+    int br = r;
+    if constexpr (EPI == 1) {  // rows of W1|W3: 64 gate rows then the 64 matching up rows per wave half
+      const int f = (r >> 4) & 7;
+      br = (f >= 4 ? ep.F : 0) + (r >> 7) * 64 + (f & 3) * 16 + (r & 15);
+    }
+    offb[i] = (uint32_t)(((long)br * ldb + c * 8) * (long)sizeof(T));
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) T*)smem;
+  const uint32_t ldsw = __builtin_amdgcn_readfirstlane(lds0 + wid * 1024);  // this wave's DMA base
+
+  // fragment reads: row (l & 15) of the 16-row block, chunk (l >> 4) at its swizzled slot
+  const int fo = (lane & 15) * 64 + (((lane >> 4) ^ swz(lane & 15)) * 16);
+  const int foa = fo + 8192 * wm, fob = fo + 8192 * wn;  // wave's 128 rows = 8 blocks of 1 KiB
+  auto frag = [&](const T* tile, int off) __attribute__((always_inline)) -> V8<T> {
+    return *reinterpret_cast<const V8<T>*>(reinterpret_cast<const char*>(tile) + off);
+  };
+
+  f32x4 acc[8][8];
+  V8<T> fa0[8], fb0[8], fa1[8], fb1[8];
+
+  auto run = [&](long m0, long n0, int k0, int k1) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const T* Ab = A + m0 * lda;
+    const T* Bb = B + (EPI == 1 ? n0 / 2 : n0) * ldb;  // EPI 1: 128 features per 256-row tile
+    auto dma = [&](int s, int kt, int u) __attribute__((always_inline)) {
+      const int i = u >> 1;
+      const uint32_t lds = ldsw + (uint32_t)((s * 2 * TILE + (u & 1) * TILE) * sizeof(T) + i * 4 * 1024);
+      const T* g = (u & 1) ? Bb + (long)kt * BK : Ab + (long)kt * BK;
+      dma16s(g, (u & 1) ? offb[i] : offa[i], lds);
+    };
+#pragma unroll
+    for (int p = 0; p < NS - 1; ++p)
+#pragma unroll
+      for (int u = 0; u < 2 * NI; ++u) dma(p, min(k0 + p, k1 - 1), u);
+    wait_vm<2 * NI * (NS - 2)>();  // stage k0 landed; the younger stages stay in flight
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {
+      fa0[f] = frag(smem, foa + 1024 * f);
+      fb0[f] = frag(smem + TILE, fob + 1024 * f);
+    }
+    // step kt (slot s, fragments in ca/cb): m-blocks 0..3 (32 MFMAs); counted wait + barrier
+    // publish stage kt + 1 and free the slot of stage kt - 1; m-blocks 4..7 in 8 groups of 4
+    // MFMAs, each with 2 fragment reads of stage kt + 1 and one DMA instruction of stage kt + 4.
+    auto step = [&](auto s_c, V8<T>(&ca)[8], V8<T>(&cb)[8], V8<T>(&na)[8], V8<T>(&nb)[8], int kt) {
+      constexpr int s = decltype(s_c)::value % NS, sn = (s + 1) % NS, sd = (s + NS - 1) % NS;
+      const T* nta = smem + sn * 2 * TILE;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = mfma16(cb[j], ca[i], acc[i][j]);
+      wait_vm<2 * NI * (NS - 3)>();  // stage kt + 1 landed
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const int kd = min(kt + NS - 1, k1 - 1);
+#pragma unroll
+      for (int gi = 0; gi < 8; ++gi) {
+        na[gi] = frag(nta, foa + 1024 * gi);
+        nb[gi] = frag(nta + TILE, fob + 1024 * gi);
+        const int i = 4 + (gi >> 1);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int j = 4 * (gi & 1) + jj;
+          acc[i][j] = mfma16(cb[j], ca[i], acc[i][j]);
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        dma(sd, kd, gi);
+      }
+    };
+    constexpr int UNR = 10;  // lcm(NS, 2): compile-time ring slot and fragment register set
+    for (int kt = k0; kt < k1; kt += UNR) {
+      auto st = [&](auto j_c) __attribute__((always_inline)) {
+        constexpr int j = decltype(j_c)::value;
+        if (kt + j < k1) {
+          if constexpr (j % 2 == 0)
+            step(IC<j>{}, fa0, fb0, fa1, fb1, kt + j);
+          else
+            step(IC<j>{}, fa1, fb1, fa0, fb0, kt + j);
+        }
+      };
+      st(IC<0>{}); st(IC<1>{}); st(IC<2>{}); st(IC<3>{}); st(IC<4>{});
+      st(IC<5>{}); st(IC<6>{}); st(IC<7>{}); st(IC<8>{}); st(IC<9>{});
+    }
+    // no LDS-DMA may land after this point, and no wave may still read a slot the next
+    // prologue overwrites
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+
+  // epilogue: lane holds row m0 + 128 wm + 16 i + (l & 15), columns n0 + 128 wn + 16 j + 4 (l >> 4) + 0..3
+  const int l16 = lane & 15, g4 = lane >> 4;
+  auto store_c = [&](long m0, long n0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const long row = m0 + 128 * wm + 16 * i + l16;
+      if constexpr (EPI == 0 || EPI == 3) {
+        T* rowp = C + row * ldc + n0 + 128 * wn + 4 * g4;
+        int pos = 0;
+        if constexpr (EPI == 3) pos = (int)(row % ep.S);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+          if constexpr (EPI == 3) {
+            const int col = (int)n0 + 128 * wn + 16 * j + 4 * g4;
+            if (col < ep.nrot) {
+              const float4 cs = *reinterpret_cast<const float4*>(ep.tab + (long)pos * (ep.D / 2) + (col % ep.D) / 2);
+              float a0 = rnd16<T>(v[0]), b0 = rnd16<T>(v[1]), a1 = rnd16<T>(v[2]), b1 = rnd16<T>(v[3]);
+              rot_pair(a0, b0, cs.x, cs.y, v[0], v[1]);
+              rot_pair(a1, b1, cs.z, cs.w, v[2], v[3]);
+            }
+          }
+          *reinterpret_cast<uint2*>(rowp + 16 * j) = make_uint2(pack_x2<T>(v[0], v[1]), pack_x2<T>(v[2], v[3]));
+        }
+      } else if constexpr (EPI == 1) {
+        // features f0 + 16 j + 4 g4 + 0..3 (j < 4): gate in acc[i][j], up in acc[i][j + 4]
+        const long f0 = n0 / 2 + 64 * wn + 4 * g4;
+        T* gp = C + row * ldc + f0;
+        T* up = gp + ep.F;
+        T* ap = ep.c2 + row * ep.ldc2 + f0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float g[4], u[4], a[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            g[e] = rnd16<T>(acc[i][j][e]);
+            u[e] = rnd16<T>(acc[i][j + 4][e]);
+            a[e] = rnd16<T>(silu_f(g[e])) * u[e];
+          }
+          *reinterpret_cast<uint2*>(gp + 16 * j) = make_uint2(pack_x2<T>(g[0], g[1]), pack_x2<T>(g[2], g[3]));
+          *reinterpret_cast<uint2*>(up + 16 * j) = make_uint2(pack_x2<T>(u[0], u[1]), pack_x2<T>(u[2], u[3]));
+          *reinterpret_cast<uint2*>(ap + 16 * j) = make_uint2(pack_x2<T>(a[0], a[1]), pack_x2<T>(a[2], a[3]));
+        }
+      } else {  // EPI == 2: dg = silu'(g) * round(da * u), du = round(da * round(silu(g))) in place over gu
+        T* gp = C + row * ldc + n0 + 128 * wn + 4 * g4;
+        T* up = gp + ep.F;
+        uint2 gw[8], uw[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {  // all loads first: one wait for the whole row block
+          gw[j] = *reinterpret_cast<const uint2*>(gp + 16 * j);
+          uw[j] = *reinterpret_cast<const uint2*>(up + 16 * j);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float g[4], u[4], og[4], ou[4];
+          unpack4<T>(gw[j], g);
+          unpack4<T>(uw[j], u);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float d = rnd16<T>(acc[i][j][e]);
+            const float sg = 1.f / (1.f + __expf(-g[e]));
+            const float a = rnd16<T>(g[e] * sg);
+            const float dd = rnd16<T>(d * u[e]);
+            ou[e] = d * a;
+            og[e] = dd * sg * (1.f + g[e] * (1.f - sg));
+          }
+          *reinterpret_cast<uint2*>(gp + 16 * j) = make_uint2(pack_x2<T>(og[0], og[1]), pack_x2<T>(og[2], og[3]));
+          *reinterpret_cast<uint2*>(up + 16 * j) = make_uint2(pack_x2<T>(ou[0], ou[1]), pack_x2<T>(ou[2], ou[3]));
+        }
+      }
+    }
+  };
+
+  const int ndp = nwg - n_split;  // whole tiles first, then n_split tiles x S split units
+  const bool split = (int)blockIdx.x >= ndp;
+  int lin, k0 = 0, k1 = nk, part = 0, st = 0;
+  if (!split) {
+    lin = xcd_remap(blockIdx.x, ndp);
+  } else {
+    const int u = xcd_remap((int)blockIdx.x - ndp, n_split * S);
+    part = u / n_split;
+    st = u % n_split;
+    lin = ndp + st;
+    k0 = (int)((long)nk * part / S);
+    k1 = (int)((long)nk * (part + 1) / S);
+  }
+  long m0, n0;
+  tile_origin(lin, tiles_m, tiles_n, m0, n0);
+  run(m0, n0, k0, k1);
+  if (split) {
+    // fp32 partial in register order (thread t's register r at r * NTH + t); the last arriver of
+    // the tile sums the S partials in part order and runs the epilogue (deterministic)
+    float* w = ws + ((long)st * S + part) * (BM * BN);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[((i * 8 + j) * 4 + e) * NTH + tid] = acc[i][j][e];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* last = reinterpret_cast<int*>(smem);  // the one LDS array (free after run)
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int ticket = __hip_atomic_fetch_add(tickets + st, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *last = ticket == S - 1;
+      if (ticket == S - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    __syncthreads();
+    if (!*last) return;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int p = 0; p < S; ++p) {
+      const float* wp = ws + ((long)st * S + p) * (BM * BN);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][j][e] += wp[((i * 8 + j) * 4 + e) * NTH + tid];
+    }
+  }
+  store_c(m0, n0);
+}
+
+__global__ __launch_bounds__(256) void zero_i32_kernel(int* __restrict__ p, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) p[i] = 0;
+}
+
+}  // namespace nt
+}  // namespace pra
+
+extern "C" {
+
+// fp32 partial-tile floats and tickets the split tail of an [M, N, K] NT GEMM needs (0 = none)
+long pra_gemm_nt_ws_floats(int M, int N, int K, int cus) {
+  using namespace pra::gm;
+  const int nwg = (M / BM) * (N / BN);
+  const int S = pra::gemm_tail_split(nwg, cus, K / BK, 2);
+  return S > 1 ? (long)(nwg % cus) * S * BM * BN : 0;
+}
+int pra_gemm_nt_ticket_count(int M, int N, int K, int cus) {
+  using namespace pra::gm;
+  const int nwg = (M / BM) * (N / BN);
+  return pra::gemm_tail_split(nwg, cus, K / BK, 2) > 1 ? nwg % cus : 0;
+}
+
+// C = A B^T with the epilogue `epi` (see the file comment). A [M][K] (row stride lda), B [N][K]
+// (ldb), C [M][N] (ldc; EPI 1: gu [M][2F] with N = 2F, EPI 2: gu [M][2F] with N = F).
+// ws/tickets: sized by pra_gemm_nt_ws_floats / pra_gemm_nt_ticket_count (null when those are 0).
+hipError_t pra_gemm_nt(int dtype, int epi, const void* A, const void* B, void* C, int M, int N, int K, long lda,
+                       long ldb, long ldc, void* c2, long ldc2, int F, const void* tab, int S, int D, int nrot,
+                       float* ws, int* tickets, int cus, hipStream_t s) {
+  using namespace pra::gm;
+  if (M % BM || N % BN || K % BK || K <= 0 || lda % 8 || ldb % 8 || ldc % 8 || cus <= 0) return hipErrorInvalidValue;
+  if (epi < 0 || epi > 3) return hipErrorInvalidValue;
+  if (epi == 1 && (N != 2 * F || F % 128 || c2 == nullptr || ldc2 % 8)) return hipErrorInvalidValue;
+  if (epi == 2 && (F != N || ldc < 2L * F)) return hipErrorInvalidValue;
+  if (epi == 3 && (tab == nullptr || S <= 0 || D % 8 || D <= 0 || nrot % D || nrot > N)) return hipErrorInvalidValue;
+  // per-lane DMA offsets are 32-bit byte offsets from the tile's row base
+  const long brows = epi == 1 ? (long)F + 128 : 256;
+  if (255L * lda * 2 + 2L * K > 0xffffffffL || brows * ldb * 2 + 2L * K > 0xffffffffL) return hipErrorInvalidValue;
+  const int nwg = (M / BM) * (N / BN);
+  const int Ssplit = pra::gemm_tail_split(nwg, cus, K / BK, 2);
+  const int n_split = Ssplit > 1 && ws && tickets ? nwg % cus : 0;
+  const int Sx = n_split ? Ssplit : 1;
+  if (n_split)
+    hipLaunchKernelGGL(pra::nt::zero_i32_kernel, dim3((n_split + 255) / 256), dim3(256), 0, s, tickets, n_split);
+  const dim3 grid(nwg - n_split + n_split * Sx), block(NTH);
+#define PRA_NT_LAUNCH(TT, E)                                                                                  \
+  {                                                                                                           \
+    pra::nt::Epi<TT> ep{(TT*)c2, ldc2, F, (const float2*)tab, S, D, nrot};                                    \
+    hipLaunchKernelGGL((pra::nt::gemm_nt_kernel<TT, E>), grid, block, 0, s, (const TT*)A, (const TT*)B, (TT*)C, \
+                       M, N, K, lda, ldb, ldc, ep, ws, tickets, n_split, Sx);                                 \
+  }
+#define PRA_NT_EPI(TT)                   \
+  switch (epi) {                         \
+    case 0: PRA_NT_LAUNCH(TT, 0) break;  \
+    case 1: PRA_NT_LAUNCH(TT, 1) break;  \
+    case 2: PRA_NT_LAUNCH(TT, 2) break;  \
+    default: PRA_NT_LAUNCH(TT, 3) break; \
+  }
+  if (dtype == pra::kBF16) {
+    PRA_NT_EPI(__bf16)
+  } else if (dtype == pra::kF16) {
+    PRA_NT_EPI(_Float16)
+  } else {
+    return hipErrorInvalidValue;
+  }
+#undef PRA_NT_EPI
+#undef PRA_NT_LAUNCH
+  return hipGetLastError();
+}
+
+}  // extern "C"

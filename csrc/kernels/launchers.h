@@ -39,9 +39,17 @@ hipError_t pra_transpose16(const void* src, void* dst, long R, long C, long ld_s
 // C[M][N] (+)= A^T B, A [K][M], B [K][N] row-major (weight gradient on row-major activations);
 // M, N multiples of 256, K of 32 (gemm_wgrad.hip)
 hipError_t pra_wgrad_gemm(int dtype, const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb,
-                          long ldc, int accumulate, float* ws, int* tickets, hipStream_t s);
-long pra_wgrad_ws_floats();
-int pra_wgrad_ticket_count();
+                          long ldc, int accumulate, float* ws, int* tickets, int cus, hipStream_t s);
+long pra_wgrad_ws_floats(int M, int N, int K, int cus);
+int pra_wgrad_ticket_count(int M, int N, int K, int cus);
+// C = A B^T, A [M][K], B [N][K] (both K-contiguous) with a fused epilogue (gemm_nt.hip):
+// epi 0 plain, 1 SwiGLU forward (C = gu [M][2F], c2 = a [M][F]), 2 SwiGLU backward in place over
+// gu (C), 3 RoPE on the first nrot columns (tab float2 [S][D/2])
+hipError_t pra_gemm_nt(int dtype, int epi, const void* A, const void* B, void* C, int M, int N, int K, long lda,
+                       long ldb, long ldc, void* c2, long ldc2, int F, const void* tab, int S, int D, int nrot,
+                       float* ws, int* tickets, int cus, hipStream_t s);
+long pra_gemm_nt_ws_floats(int M, int N, int K, int cus);
+int pra_gemm_nt_ticket_count(int M, int N, int K, int cus);
 
 hipError_t pra_xent_fwd(int dtype, const void* logits, const int64_t* labels, float* lse, float* loss_row,
                         float* stats, long T, long V, long ld, long ignore_index, hipStream_t s);

@@ -1,8 +1,10 @@
 """Fused autograd ops of the Transformer hot path.
 
 Each op runs the HIP kernels of ``pyrecover_amd._C`` for GPU tensors and the plain-torch math of
-:mod:`pyrecover_amd.ops.reference` for CPU tensors (CPU/gloo runs only). GEMMs are plain
-library GEMMs (``torch.mm`` -> hipBLASLt on ROCm); everything between them is ours.
+:mod:`pyrecover_amd.ops.reference` for CPU tensors (CPU/gloo runs only). GEMMs run on the
+hand-written MFMA kernels (csrc/kernels/gemm_nt.hip for forward / data gradients, with RoPE and
+SwiGLU fused into their epilogues; gemm_wgrad.hip for weight gradients) wherever their shape rules
+and the site selection allow, else on the library (``torch.mm`` -> hipBLASLt).
 
 Weight gradients are produced directly into *gradient slots* (:mod:`pyrecover_amd.parallel.flat`)
 instead of being returned to autograd, so they land in the flat gradient buffer / DDP bucket
@@ -133,15 +135,20 @@ WGRAD_AUTO = os.environ.get("PYRECOVER_WGRAD", "auto") == "auto"
 WGRAD_AUTO_MIN_TOKENS = 16384
 
 
-def _hip_wgrad_dims(t, site, tokens, *cols) -> bool:
-    """The MFMA weight-gradient kernel's shape rules: K = tokens % 32, every output dim % 256."""
-    return (site in WGRAD_SITES and _ext.hip16(t) and tokens % 32 == 0 and tokens > 0
-            and (not WGRAD_AUTO or tokens >= WGRAD_AUTO_MIN_TOKENS) and all(c % 256 == 0 for c in cols))
+def _hip_wgrad_dims(t, site, tokens, *cols, force=False) -> bool:
+    """The MFMA weight-gradient kernel's shape rules: K = tokens % 32, every output dim % 256.
+    `force`: the operands exist only row-major (no transposed copy to hand the library), so the
+    kernel runs whatever the site list and token threshold say (PYRECOVER_WGRAD=lib still wins)."""
+    if WGRAD_SITES == _WGRAD_SITE_SETS["lib"] and os.environ.get("PYRECOVER_WGRAD") == "lib":
+        force = False
+    return ((force or (site in WGRAD_SITES and (not WGRAD_AUTO or tokens >= WGRAD_AUTO_MIN_TOKENS)))
+            and _ext.hip16(t) and tokens % 32 == 0 and tokens > 0 and all(c % 256 == 0 for c in cols))
 
 
-def _hip_wgrad_ok(dy2, x2, site) -> bool:
+def _hip_wgrad_ok(dy2, x2, site, force=False) -> bool:
     return (dy2.dim() == 2 and x2.dim() == 2 and dy2.dtype == x2.dtype and dy2.device == x2.device
-            and dy2.size(0) == x2.size(0) and _hip_wgrad_dims(dy2, site, dy2.size(0), dy2.size(1), x2.size(1))
+            and dy2.size(0) == x2.size(0)
+            and _hip_wgrad_dims(dy2, site, dy2.size(0), dy2.size(1), x2.size(1), force=force)
             and all(t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0 for t in (dy2, x2)))
 
 
@@ -157,15 +164,78 @@ def _hip_wgrad(slot, dy2, x2, shape):
         slot.end(buf)
 
 
-def _wgrad_into(slot, dy2, x2, shape, site):
+def _wgrad_into(slot, dy2, x2, shape, site, force=False):
     """slot <- dy2^T x2 (dy2 [T, out], x2 [T, in]); `site` names the projection (WGRAD_SITES)."""
-    if _hip_wgrad_ok(dy2, x2, site):
+    if _hip_wgrad_ok(dy2, x2, site, force):
         _hip_wgrad(slot, dy2, x2, shape)
     elif TN_WGRAD and _tn_ok(dy2) and _tn_ok(x2):
         C = _ext.require_for(dy2)
         slot.mm_(C.transpose2d(dy2), C.transpose2d(x2).t(), shape)
     else:
         slot.mm_(dy2.t(), x2, shape)
+
+
+# Forward and data-gradient GEMMs on the hand-written MFMA NT kernel (csrc/kernels/gemm_nt.hip):
+# both operands K-contiguous (activations [T, in] x weights [out, in]; the data gradients use the
+# transposed weight shadows), with fused epilogues where a separate memory-bound pass followed:
+# RoPE on the QKV projection, SwiGLU on the W1|W3 projection, the SwiGLU backward on the W2 data
+# gradient. PYRECOVER_GEMM: "auto" (default: every site whose tile grid fills >= 2 rounds of the
+# CUs, where the 256 x 256 tile pays), "hip" (every valid site), "lib" (hipBLASLt everywhere), or
+# a comma list of sites: forward qkv, o, w13, w2, head; data gradient qkv_d, o_d, w13_d, w2_d, head_d.
+_NT_ALL = frozenset({"qkv", "o", "w13", "w2", "head", "qkv_d", "o_d", "w13_d", "w2_d", "head_d"})
+
+
+def _gemm_sites(v: str) -> frozenset:
+    if v in ("auto", "hip"):
+        return _NT_ALL
+    if v == "lib":
+        return frozenset()
+    sites = frozenset(x.strip() for x in v.split(",") if x.strip())
+    bad = sites - _NT_ALL
+    if bad:
+        raise ValueError(f"PYRECOVER_GEMM: unknown site(s) {sorted(bad)}")
+    return sites
+
+
+GEMM_SITES = _gemm_sites(os.environ.get("PYRECOVER_GEMM", "auto"))
+GEMM_AUTO = os.environ.get("PYRECOVER_GEMM", "auto") == "auto"
+_CUS = {}
+
+
+def _cus(t) -> int:
+    i = t.device.index
+    if i not in _CUS:
+        _CUS[i] = torch.cuda.get_device_properties(t.device).multi_processor_count
+    return _CUS[i]
+
+
+def _nt_ok(a, b, site) -> bool:
+    """out = a b^T on the NT kernel: a [M, K], b [N, K] K-contiguous 16-bit, M, N % 256, K % 32."""
+    if site not in GEMM_SITES or b is None or not _ext.hip16(a):
+        return False
+    if not (a.dim() == 2 and b.dim() == 2 and a.dtype == b.dtype and a.device == b.device
+            and a.size(1) == b.size(1) and a.size(0) % 256 == 0 and b.size(0) % 256 == 0 and a.size(1) % 32 == 0):
+        return False
+    if not all(t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0 for t in (a, b)):
+        return False
+    return not GEMM_AUTO or (a.size(0) // 256) * (b.size(0) // 256) >= 2 * _cus(a)
+
+
+def _mm_nt(a, b, site, b_t=None):
+    """a @ b^T. `b_t` (optional) is b^T stored K-contiguous the other way round: when the NT
+    kernel cannot run, the library GEMM uses whichever layout it has."""
+    if _nt_ok(a, b, site):
+        out = torch.empty(a.size(0), b.size(0), dtype=a.dtype, device=a.device)
+        _ext.require_for(a).gemm_nt_(a, b, out)
+        return out
+    return torch.mm(a, b_t) if b_t is not None else torch.mm(a, b.t())
+
+
+def _mm_dgrad(dy, w, w_t, site):
+    """dX = dY W (w [out, in]); w_t = W^T [in, out] is the K-contiguous shadow the NT kernel reads."""
+    if w_t is not None:
+        return _mm_nt(dy, w_t, site)
+    return torch.mm(dy, w)
 
 
 # ---------------------------------------------------------------------------------------
@@ -345,19 +415,24 @@ class _AttentionBlock(torch.autograd.Function):
         T = B * S
         dim = x.shape[-1]
         x2 = x.reshape(T, dim)
-        qkv = torch.mm(x2, w_qkv.t())
         nq, nk = Hq * D, Hkv * D
-        if _ext.hip(qkv) and D % 8 == 0:
-            _ext.require_for(qkv).rope_(qkv, nq + nk, tab, D, S, 0, False)
+        if _nt_ok(x2, w_qkv, "qkv") and D % 8 == 0 and T % S == 0 and tab.is_contiguous():
+            # QKV projection with RoPE on q and k in the GEMM epilogue
+            qkv = torch.empty(T, w_qkv.size(0), dtype=x2.dtype, device=x2.device)
+            _ext.require_for(x2).gemm_nt_(x2, w_qkv, qkv, 3, None, tab, S, D, nq + nk)
         else:
-            ref.rope_inplace_2d(qkv, nq + nk, tab, D, S)
+            qkv = torch.mm(x2, w_qkv.t())
+            if _ext.hip(qkv) and D % 8 == 0:
+                _ext.require_for(qkv).rope_(qkv, nq + nk, tab, D, S, 0, False)
+            else:
+                ref.rope_inplace_2d(qkv, nq + nk, tab, D, S)
         q = qkv[:, :nq].view(B, S, Hq, D)
         k = qkv[:, nq:nq + nk].view(B, S, Hkv, D)
         v = qkv[:, nq + nk:].view(B, S, Hkv, D)
         scale = 1.0 / math.sqrt(D)
         o, lse = _attn_fwd(q, k, v, scale, causal)
         o2 = o.view(T, nq)
-        y = torch.mm(o2, w_o.t())
+        y = _mm_nt(o2, w_o, "o")
         ctx.save_for_backward(x2, qkv, o, lse, w_qkv, w_o, tab)
         ctx.slots = (slot_qkv, slot_o)
         ctx.dims = dims
@@ -376,7 +451,7 @@ class _AttentionBlock(torch.autograd.Function):
         # every read of a weight is enqueued BEFORE its gradient slot is published: a published
         # slot may be updated by the optimizer (overlapped with backward) on another stream.
         w_qkv_t, w_o_t = ctx.w_t if ctx.w_t is not None else (None, None)
-        do = (torch.mm(dy2, w_o_t.t()) if w_o_t is not None else torch.mm(dy2, w_o)).view(B, S, Hq, D)
+        do = _mm_dgrad(dy2, w_o, w_o_t, "o_d").view(B, S, Hq, D)
         if TN_WGRAD_WO:
             _wgrad_into(slot_o, dy2, o2, tuple(w_o.shape), "o")
         else:
@@ -394,14 +469,14 @@ class _AttentionBlock(torch.autograd.Function):
             # inverse RoPE in place + dqkv^T in one pass, for the K-contiguous weight-grad GEMM
             C = _ext.require_for(dqkv)
             dqkvT = C.rope_t_(dqkv, nq + nk, tab, D, S, True)
-            dx = torch.mm(dqkv, w_qkv_t.t()) if w_qkv_t is not None else torch.mm(dqkv, w_qkv)
+            dx = _mm_dgrad(dqkv, w_qkv, w_qkv_t, "qkv_d")
             slot_qkv.mm_(dqkvT, C.transpose2d(x2).t(), tuple(w_qkv.shape))
         else:
             if _ext.hip(dqkv) and D % 8 == 0:
                 _ext.require_for(dqkv).rope_(dqkv, nq + nk, tab, D, S, 0, True)
             else:
                 ref.rope_inplace_2d(dqkv, nq + nk, tab, D, S, inverse=True)
-            dx = torch.mm(dqkv, w_qkv_t.t()) if w_qkv_t is not None else torch.mm(dqkv, w_qkv)
+            dx = _mm_dgrad(dqkv, w_qkv, w_qkv_t, "qkv_d")
             _wgrad_into(slot_qkv, dqkv, x2, tuple(w_qkv.shape), "qkv")
         n_params = ctx.needs_input_grad.__len__() - 8
         return (dx.view(B, S, -1), None, None, None, None, None, None, None) + (None,) * n_params
@@ -440,21 +515,38 @@ class _SwiGLUMLP(torch.autograd.Function):
         ctx.w_t = w_t
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
-        gu = torch.mm(x2, w13.t())
-        F = gu.shape[1] // 2
-        if (not _hip_wgrad_dims(gu, "w2", gu.shape[0], shape[-1], F) and TN_WGRAD and _tn_ok(gu)
-                and F % 64 == 0):
-            # a^T (K-contiguous operand of the W2 weight gradient) is written in the same pass and
-            # kept instead of a
-            a, a_saved = _ext.require_for(gu).swiglu_fwd_t(gu)
-            ctx.a_is_t = True
-        else:
-            a = a_saved = _swiglu_fwd(gu)
+        F = w13.shape[0] // 2
+        ctx.fused_act = False
+        if _nt_ok(x2, w13, "w13") and F % 128 == 0:
+            # W1|W3 projection with the SwiGLU epilogue: writes gu (kept for the backward) and a
+            gu = torch.empty(x2.size(0), 2 * F, dtype=x2.dtype, device=x2.device)
+            a = a_saved = torch.empty(x2.size(0), F, dtype=x2.dtype, device=x2.device)
+            _ext.require_for(x2).gemm_nt_(x2, w13, gu, 1, a)
             ctx.a_is_t = False
-        y = torch.mm(a, w2.t())
+            ctx.fused_act = True
+        else:
+            gu = torch.mm(x2, w13.t())
+            if (not _hip_wgrad_dims(gu, "w2", gu.shape[0], shape[-1], F) and TN_WGRAD and _tn_ok(gu)
+                    and F % 64 == 0):
+                # a^T (K-contiguous operand of the W2 weight gradient) is written in the same pass
+                # and kept instead of a
+                a, a_saved = _ext.require_for(gu).swiglu_fwd_t(gu)
+                ctx.a_is_t = True
+            else:
+                a = a_saved = _swiglu_fwd(gu)
+                ctx.a_is_t = False
+        y = _mm_nt(a, w2, "w2")
         ctx.save_for_backward(x2, gu, a_saved, w13, w2)
         ctx.slots = (slot13, slot2)
         return y.view(shape)
+
+    @staticmethod
+    def _w2_wgrad(ctx, slot2, dy2, a, w2):
+        if ctx.a_is_t:  # TN weight gradient: dW2 = (dY^T) (a^T)^T, both operands K-contiguous
+            dyT = _ext.require_for(dy2).transpose2d(dy2) if _tn_ok(dy2) else dy2.t()
+            slot2.mm_(dyT, a.t(), tuple(w2.shape))
+        else:  # a exists only row-major after the fused SwiGLU epilogue: the MFMA kernel reads it as is
+            _wgrad_into(slot2, dy2, a, tuple(w2.shape), "w2", force=ctx.fused_act)
 
     @staticmethod
     def backward(ctx, dy):
@@ -463,25 +555,32 @@ class _SwiGLUMLP(torch.autograd.Function):
         shape = dy.shape
         dy2 = dy.reshape(-1, shape[-1])
         w13_t, w2_t = ctx.w_t if ctx.w_t is not None else (None, None)
-        da = torch.mm(dy2, w2_t.t()) if w2_t is not None else torch.mm(dy2, w2)
-        if ctx.a_is_t:  # TN weight gradient: dW2 = (dY^T) (a^T)^T, both operands K-contiguous
-            dyT = _ext.require_for(dy2).transpose2d(dy2) if _tn_ok(dy2) else dy2.t()
-            slot2.mm_(dyT, a.t(), tuple(w2.shape))
-        else:
-            _wgrad_into(slot2, dy2, a, tuple(w2.shape), "w2")
+        F = gu.shape[1] // 2
+        if _nt_ok(dy2, w2_t, "w2_d") and F % 256 == 0:
+            # W2 data gradient with the SwiGLU backward in the epilogue: da never leaves the
+            # registers; g, u in gu are overwritten with dg, du
+            _ext.require_for(dy2).gemm_nt_(dy2, w2_t, gu, 2)
+            _SwiGLUMLP._w2_wgrad(ctx, slot2, dy2, a, w2)
+            dgu = gu
+            dx = _mm_dgrad(dgu, w13, w13_t, "w13_d")
+            _wgrad_into(slot13, dgu, x2, tuple(w13.shape), "w13", force=True)
+            n_params = len(ctx.needs_input_grad) - 6
+            return (dx.view(shape), None, None, None, None, None) + (None,) * n_params
+        da = _mm_dgrad(dy2, w2, w2_t, "w2_d")
+        _SwiGLUMLP._w2_wgrad(ctx, slot2, dy2, a, w2)
         if _hip_wgrad_ok(gu, x2, "w13"):
             dgu = _swiglu_bwd_(da, gu)  # in place over gu; no transposed copy for the MFMA wgrad
-            dx = torch.mm(dgu, w13_t.t()) if w13_t is not None else torch.mm(dgu, w13)
+            dx = _mm_dgrad(dgu, w13, w13_t, "w13_d")
             _hip_wgrad(slot13, dgu, x2, tuple(w13.shape))
         elif TN_WGRAD and _tn_ok(gu) and _tn_ok(x2) and _tn_ok(da):
             # SwiGLU backward in place over gu, writing dgu^T in the same pass
             C = _ext.require_for(gu)
             dguT = C.swiglu_bwd_t_(da, gu)
-            dx = torch.mm(gu, w13_t.t()) if w13_t is not None else torch.mm(gu, w13)
+            dx = _mm_dgrad(gu, w13, w13_t, "w13_d")
             slot13.mm_(dguT, C.transpose2d(x2).t(), tuple(w13.shape))
         else:
             dgu = _swiglu_bwd_(da, gu)  # in place over gu (dead after this)
-            dx = torch.mm(dgu, w13_t.t()) if w13_t is not None else torch.mm(dgu, w13)
+            dx = _mm_dgrad(dgu, w13, w13_t, "w13_d")
             _wgrad_into(slot13, dgu, x2, tuple(w13.shape), "w13")
         n_params = len(ctx.needs_input_grad) - 6
         return (dx.view(shape), None, None, None, None, None) + (None,) * n_params
@@ -503,7 +602,7 @@ class _LinearCrossEntropy(torch.autograd.Function):
         ctx.w_t = w_t
         h2 = h.reshape(-1, h.shape[-1])
         lab = labels.reshape(-1).contiguous()
-        logits = torch.mm(h2, w_out.t())
+        logits = _mm_nt(h2, w_out, "head")
         if _ext.hip(logits):
             lse, _, stats = _ext.require_for(logits).xent_fwd(logits, lab, ignore_index)
             loss = stats[0]
@@ -531,7 +630,7 @@ class _LinearCrossEntropy(torch.autograd.Function):
             p[torch.arange(lab.numel(), device=p.device), lab.clamp_min(0)] -= valid.to(p.dtype)
             p = p * valid.to(p.dtype).unsqueeze(1) * (dloss.to(p.dtype) / n)
             dlogits = p.to(logits.dtype)
-        dh = torch.mm(dlogits, ctx.w_t.t()) if ctx.w_t is not None else torch.mm(dlogits, w_out)
+        dh = _mm_dgrad(dlogits, w_out, ctx.w_t, "head_d")
         _wgrad_into(ctx.slot, dlogits, h2, tuple(w_out.shape), "head")
         return dh.view(ctx.hshape), None, None, None, None, None, None
 

@@ -28,16 +28,31 @@ def ref_forward(m, tok):
     return h @ m.output.weight.t()
 
 
-@pytest.mark.parametrize("preset,over,dtype", [("llama-micro", {}, torch.bfloat16), ("llama-tiny", {}, torch.bfloat16),
-                                               # FFN 768: every weight gradient on the MFMA wgrad kernel
-                                               ("llama-tiny", {"multiple_of": 256}, torch.bfloat16),
-                                               ("gpt2-small", {"n_layers": 2, "vocab_size": 1024}, torch.bfloat16),
-                                               ("llama-tiny", {"n_kv_heads": 2}, torch.float16),
-                                               ("llama-micro", {}, torch.float32),
-                                               ("llama-micro", {}, torch.float64)])
-def test_model_grads_vs_fp32_reference(cuda, preset, over, dtype):
+@pytest.mark.parametrize("preset,over,dtype,kernels", [
+    ("llama-micro", {}, torch.bfloat16, "auto"), ("llama-tiny", {}, torch.bfloat16, "auto"),
+    # FFN a multiple of 256: every GEMM on the hand-written MFMA kernels (NT forward / data gradients
+    # with the RoPE / SwiGLU / SwiGLU-backward epilogues, weight gradients), below the auto thresholds
+    ("llama-tiny", {"multiple_of": 256}, torch.bfloat16, "mfma"),
+    ("llama-tiny", {"multiple_of": 256}, torch.bfloat16, "lib"),
+    ("gpt2-small", {"n_layers": 2, "vocab_size": 1024}, torch.bfloat16, "mfma"),
+    ("gpt2-small", {"n_layers": 2, "vocab_size": 1024}, torch.bfloat16, "auto"),
+    ("llama-tiny", {"n_kv_heads": 2, "multiple_of": 256}, torch.float16, "mfma"),
+    ("llama-micro", {}, torch.float32, "auto"),
+    ("llama-micro", {}, torch.float64, "auto")])
+def test_model_grads_vs_fp32_reference(cuda, monkeypatch, preset, over, dtype, kernels):
     """Every --model-dtype trains on the GPU: bf16/fp16 on the HIP kernels, fp32 on the HIP
-    element-wise kernels + torch attention, fp64 on torch math (reference utils.py:11-16)."""
+    element-wise kernels + torch attention, fp64 on torch math (reference utils.py:11-16).
+    kernels="mfma" forces every GEMM site onto the hand-written MFMA GEMMs, "lib" onto hipBLASLt."""
+    from pyrecover_amd.ops import fused
+
+    if kernels == "mfma":
+        monkeypatch.setattr(fused, "GEMM_AUTO", False)
+        monkeypatch.setattr(fused, "GEMM_SITES", fused._NT_ALL)
+        monkeypatch.setattr(fused, "WGRAD_AUTO", False)
+        monkeypatch.setattr(fused, "WGRAD_SITES", fused._WGRAD_SITE_SETS["hip"])
+    elif kernels == "lib":
+        monkeypatch.setattr(fused, "GEMM_SITES", frozenset())
+        monkeypatch.setattr(fused, "WGRAD_SITES", frozenset())
     torch.manual_seed(0)
     a = get_preset(preset, seq_len=256, **over)
     cpu = Transformer(a)
