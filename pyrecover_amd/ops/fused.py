@@ -179,14 +179,20 @@ def _wgrad_into(slot, dy2, x2, shape, site, force=False):
 # both operands K-contiguous (activations [T, in] x weights [out, in]; the data gradients use the
 # transposed weight shadows), with fused epilogues where a separate memory-bound pass followed:
 # RoPE on the QKV projection, SwiGLU on the W1|W3 projection, the SwiGLU backward on the W2 data
-# gradient. PYRECOVER_GEMM: "auto" (default: every site whose tile grid fills >= 2 rounds of the
-# CUs, where the 256 x 256 tile pays), "hip" (every valid site), "lib" (hipBLASLt everywhere), or
-# a comma list of sites: forward qkv, o, w13, w2, head; data gradient qkv_d, o_d, w13_d, w2_d, head_d.
+# gradient. The kernel runs at 0.85-0.88 of hipBLASLt on the 7B shapes (1.35-1.40 vs 1.55-1.64
+# PF), which the fused epilogues do not win back (W1|W3 + SwiGLU 4.52 vs 4.09 ms, W2 data grad +
+# SwiGLU backward 2.77 vs 2.49 ms; profiles/gemm_nt_r3.md), so "auto" keeps every NT site on
+# hipBLASLt. PYRECOVER_GEMM: "auto" (default), "hip" (every valid site on the NT kernel), "lib",
+# or a comma list of sites: forward qkv, o, w13, w2, head; data gradient qkv_d, o_d, w13_d, w2_d,
+# head_d.
 _NT_ALL = frozenset({"qkv", "o", "w13", "w2", "head", "qkv_d", "o_d", "w13_d", "w2_d", "head_d"})
+_NT_AUTO = frozenset()
 
 
 def _gemm_sites(v: str) -> frozenset:
-    if v in ("auto", "hip"):
+    if v == "auto":
+        return _NT_AUTO
+    if v == "hip":
         return _NT_ALL
     if v == "lib":
         return frozenset()

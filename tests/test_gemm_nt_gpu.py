@@ -27,7 +27,7 @@ def _rel_err(out, ref):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("M,N,K", [(256, 256, 32), (512, 768, 256), (1024, 512, 1056),
+@pytest.mark.parametrize("M,N,K", [(256, 256, 32), (512, 768, 256), (1024, 512, 1056), (512, 512, 4160),
                                    (4096, 4352, 128),  # 272 tiles: split-K tail (S = 2)
                                    (2048, 256 * 33, 96)])
 def test_gemm_nt_plain_matches_oracle(cuda, dtype, M, N, K):
@@ -74,8 +74,14 @@ def test_swiglu_fwd_epilogue_bitwise_vs_unfused(cuda, T, F, D):
     C.gemm_nt_(x, w13, gu, 1, a)
     gu0 = torch.empty_like(gu)
     C.gemm_nt_(x, w13, gu0)
-    assert torch.equal(gu, gu0)
-    assert torch.equal(a, C.swiglu_fwd(gu0))
+    # the epilogue's a is exactly swiglu_fwd of the gu it stored
+    assert torch.equal(a, C.swiglu_fwd(gu))
+    if (T // 256) * (2 * F // 256) <= 256:
+        assert torch.equal(gu, gu0)  # same tiles' sums, bit for bit
+    else:
+        # with a split-K tail, gate/up interleaving puts some elements in split tiles in one
+        # launch and in whole tiles in the other (fp32 sums in another order): <= 1 bf16 ulp
+        assert torch.allclose(gu.float(), gu0.float(), rtol=2 ** -7, atol=1e-6)
     # and the math itself against fp32
     ref = x.float() @ w13.float().t()
     g, u = ref[:, :F].bfloat16().float(), ref[:, F:].bfloat16().float()

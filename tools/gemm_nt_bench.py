@@ -89,6 +89,7 @@ def main():
             assert err < 1e-2, (name, err)
             del ref
             y2 = torch.empty_like(y)
+
             run_arms(name, 2.0 * T * N * K, {"lib": lambda: torch.mm(x, w.t(), out=y2), "hip": lambda: C.gemm_nt_(x, w, y)},
                      {"rel_err": round(err, 5)})
             del x, w, y, y2
