@@ -220,7 +220,7 @@ at::Tensor swiglu_fwd(const at::Tensor& gu) {
 }
 
 // dgu may alias gu (in-place backward).
-at::Tensor swiglu_bwd(const at::Tensor& dy, const at::Tensor& gu, c10::optional<at::Tensor> out) {
+at::Tensor swiglu_bwd(const at::Tensor& dy, const at::Tensor& gu, c10::optional<at::Tensor> out, int64_t variant) {
   const Range range_("pyrecover::swiglu_bwd");
   check_dev(gu, "gu");
   check_row_major(gu, "gu");
@@ -236,7 +236,7 @@ at::Tensor swiglu_bwd(const at::Tensor& dy, const at::Tensor& gu, c10::optional<
   char* o = (char*)dgu.data_ptr();
   const int64_t es = gu.element_size();
   check(pra_swiglu_bwd(dt(gu), dy.data_ptr(), g, g + F * es, o, o + F * es, gu.size(0), (int)F, (int)gu.stride(0),
-                       (int)gu.stride(0), (int)dy.stride(0), stream_of(gu)),
+                       (int)gu.stride(0), (int)dy.stride(0), (int)variant, stream_of(gu)),
         "swiglu_bwd");
   return dgu;
 }
@@ -603,7 +603,7 @@ void check_bshd(const at::Tensor& t, const char* name, int64_t B, int64_t S, int
                 at::ScalarType dtype) {
   TORCH_CHECK(t.dim() == 4 && t.size(0) == B && t.size(1) == S && t.size(2) == H && t.size(3) == D,
               "attention: ", name, " must be [B, S, H, D] = [", B, ", ", S, ", ", H, ", ", D, "], got ", t.sizes());
-  TORCH_CHECK(t.stride(3) == 1 && t.stride(2) == D && (S == 1 || t.stride(0) == S * t.stride(1)),
+  TORCH_CHECK(t.stride(3) == 1 && t.stride(2) == D && (B == 1 || S == 1 || t.stride(0) == S * t.stride(1)),
               "attention: ", name, " must have token-major layout with contiguous heads, strides ", t.strides());
   TORCH_CHECK(t.scalar_type() == dtype, "attention: ", name, " must be ", dtype, " like q");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "attention: ", name, " must be 16-B aligned");
@@ -665,7 +665,7 @@ std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const
 // Writes dq/dk/dv into caller-provided [B,S,H,D] views (e.g. slices of a fused dQKV buffer).
 void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const at::Tensor& o,
               const at::Tensor& dout, const at::Tensor& lse, at::Tensor dq, at::Tensor dk, at::Tensor dv, double scale,
-              bool causal) {
+              bool causal, c10::optional<at::Tensor> rope_tab) {
   const Range range_("pyrecover::attn_bwd");
   check_dev(q, "q");
   check_attn_dtype(q);
@@ -683,6 +683,15 @@ void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, con
   TORCH_CHECK(Hq % Hkv == 0, "attention: n_heads must be a multiple of n_kv_heads");
   TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.numel() == B * Hq * S && lse.is_contiguous(), "attention: lse");
   for (const at::Tensor& t : {k, v, o, dout, lse, dq, dk, dv}) same_dev(q, t, "attention operand");
+  // optional RoPE table [>= S, D/2, 2] fp32 (cos, sin): dq / dk are stored with the inverse rotation
+  const float* rtab = nullptr;
+  if (rope_tab.has_value()) {
+    const at::Tensor& tb = *rope_tab;
+    TORCH_CHECK(tb.scalar_type() == at::kFloat && tb.is_contiguous() && tb.numel() >= S * D &&
+                    tb.numel() % D == 0, "attention: rope table must be contiguous fp32 [>= S, D/2, 2]");
+    same_dev(q, tb, "rope table");
+    rtab = tb.data_ptr<float>();
+  }
   const c10::DeviceGuard guard(q.device());
   if (S % kSeqPad) {
     const int64_t Sp = round_up(S, kSeqPad);
@@ -697,7 +706,7 @@ void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, con
                        lp.data_ptr<float>(), delta.data_ptr<float>(), dqp.data_ptr(), dkp.data_ptr(), dvp.data_ptr(),
                        (int)B, (int)Sp, (int)Hq, (int)Hkv, (int)D, qp.stride(1), kp.stride(1), vp.stride(1),
                        op.stride(1), dop.stride(1), dqp.stride(1), dkp.stride(1), dvp.stride(1), (float)scale,
-                       causal ? 1 : 0, (int)S, nullptr, 0, stream_of(q)),
+                       causal ? 1 : 0, (int)S, rtab, stream_of(q)),
           "attn_bwd");
     dq.copy_(dqp.narrow(1, 0, S));
     dk.copy_(dkp.narrow(1, 0, S));
@@ -705,16 +714,11 @@ void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, con
     return;
   }
   at::Tensor delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
-  // dS-materializing backward: a [B, Hq, S, S] 16-bit workspace (from the caching allocator, so
-  // every layer's backward reuses the same block) when the launcher would take that path
-  const size_t ds_bytes = pra_attn_bwd_ds_bytes((int)B, (int)S, (int)Hq, (int)Hkv, (int)D, causal ? 1 : 0);
-  at::Tensor ds_ws;
-  if (ds_bytes) ds_ws = at::empty({(int64_t)(ds_bytes / 2)}, q.options());
   check(pra_attn_bwd(dt(q), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
                      lse.data_ptr<float>(), delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
                      (int)B, (int)S, (int)Hq, (int)Hkv, (int)D, q.stride(1), k.stride(1), v.stride(1), o.stride(1),
                      dout.stride(1), dq.stride(1), dk.stride(1), dv.stride(1), (float)scale, causal ? 1 : 0, (int)S,
-                     ds_bytes ? ds_ws.data_ptr() : nullptr, ds_bytes, stream_of(q)),
+                     rtab, stream_of(q)),
         "attn_bwd");
 }
 
@@ -733,7 +737,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("rope_", &rope_);
   m.def("swiglu_fwd", &swiglu_fwd);
-  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("swiglu_bwd", &swiglu_bwd, pybind11::arg("dy"), pybind11::arg("gu"), pybind11::arg("out") = pybind11::none(),
+        pybind11::arg("variant") = -1);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("xent_fwd", &xent_fwd);
@@ -755,7 +760,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("swiglu_fwd_t", &swiglu_fwd_t);
   m.def("rope_t_", &rope_t_);
   m.def("attn_fwd", &attn_fwd);
-  m.def("attn_bwd", &attn_bwd);
+  m.def("attn_bwd", &attn_bwd, pybind11::arg("q"), pybind11::arg("k"), pybind11::arg("v"), pybind11::arg("o"),
+        pybind11::arg("dout"), pybind11::arg("lse"), pybind11::arg("dq"), pybind11::arg("dk"), pybind11::arg("dv"),
+        pybind11::arg("scale"), pybind11::arg("causal"), pybind11::arg("rope_tab") = pybind11::none());
+  m.def("attn_set_options", [](int fwd_pipe, double fwd_thr, int dkdv_impl, int dq_pipe) {
+    pra_attn_set_options(fwd_pipe, (float)fwd_thr, dkdv_impl, dq_pipe);
+  }, "attention kernel selection: fwd_pipe / dkdv_impl / dq_pipe = -1 (by shape), 0 or 1; fwd_thr = rescale threshold (log2)");
   register_ckpt_engine(m);
   register_xgmi(m);
 }

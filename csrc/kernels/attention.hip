@@ -30,8 +30,6 @@
 // B1 S8192 H32/8 causal: bwd 2.68 -> 1.91 ms with the pipelined kernels (719 TF model, 1.0 PF executed).
 #include "common.h"
 
-#include <stdlib.h>
-
 #include <type_traits>
 
 namespace pra {
@@ -101,22 +99,45 @@ template <typename T>
 __device__ __forceinline__ uint32_t pack_x2(float a, float b) {
   return (uint32_t)__builtin_bit_cast(uint16_t, (T)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (T)b) << 16);
 }
+// rt (optional): this lane's row of the RoPE table (float2 (cos, sin) per column pair, the layout of
+// the RoPE kernels); the inverse rotation of each (2i, 2i+1) pair is applied to the fp32 values
+// before they are rounded (the backward's dQ / dK leave the kernel already un-rotated, so the
+// separate inverse-RoPE pass over dq|dk is gone). A pair never straddles lanes: register k (even) of
+// block db holds column 32 db + crow(k, h2), and k + 1 the next column.
+__device__ __forceinline__ void rot_inv(float& a, float& b, float c, float s) {  // (a + ib)(c - is)
+  const float o0 = __builtin_fmaf(a, c, -(b * -s));
+  const float o1 = __builtin_fmaf(a, -s, b * c);
+  a = o0;
+  b = o1;
+}
 template <typename T, int NDB>
-__device__ __forceinline__ void store_rows16(const f32x16 (&acc)[NDB], float f, T* p, bool ok, int h2) {
+__device__ __forceinline__ void store_rows16(const f32x16 (&acc)[NDB], float f, T* p, bool ok, int h2,
+                                             const float2* rt = nullptr) {
 #pragma unroll
   for (int db = 0; db < NDB; ++db)
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
       const int a = 8 * m, c = 8 * m + 4;  // register groups rr = 2m (A) and 2m + 1 (B)
-      const auto x0 = __builtin_amdgcn_permlane32_swap(pack_x2<T>(acc[db][c] * f, acc[db][c + 1] * f),
-                                                      pack_x2<T>(acc[db][a] * f, acc[db][a + 1] * f), false, false);
-      const auto x1 = __builtin_amdgcn_permlane32_swap(pack_x2<T>(acc[db][c + 2] * f, acc[db][c + 3] * f),
-                                                      pack_x2<T>(acc[db][a + 2] * f, acc[db][a + 3] * f), false, false);
+      float va[4], vc[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        va[j] = acc[db][a + j] * f;
+        vc[j] = acc[db][c + j] * f;
+      }
+      if (rt != nullptr) {  // pairs 16 db + 8 m + 2 h2 + {0, 1} (A) and + 4 (B)
+        const float4 ta = *reinterpret_cast<const float4*>(rt + 16 * db + 8 * m + 2 * h2);
+        const float4 tc = *reinterpret_cast<const float4*>(rt + 16 * db + 8 * m + 4 + 2 * h2);
+        rot_inv(va[0], va[1], ta.x, ta.y);
+        rot_inv(va[2], va[3], ta.z, ta.w);
+        rot_inv(vc[0], vc[1], tc.x, tc.y);
+        rot_inv(vc[2], vc[3], tc.z, tc.w);
+      }
+      const auto x0 = __builtin_amdgcn_permlane32_swap(pack_x2<T>(vc[0], vc[1]), pack_x2<T>(va[0], va[1]), false, false);
+      const auto x1 = __builtin_amdgcn_permlane32_swap(pack_x2<T>(vc[2], vc[3]), pack_x2<T>(va[2], va[3]), false, false);
       if (ok)
         *reinterpret_cast<uint4*>(p + 32 * db + 16 * m + 8 * (1 - h2)) = make_uint4(x0[0], x1[0], x0[1], x1[1]);
     }
 }
-
 
 // lanes i and i^32 exchange through v_permlane32_swap (no LDS round trip)
 __device__ __forceinline__ float half_max(float x) {
@@ -393,7 +414,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_kernel(const T* __restrict__ Q
 // iteration t and written into the slot tile t-1 vacated, one barrier per tile. In causal mode a
 // wave's only diagonal tile is its last one.
 // ======================================================================================
-template <typename T, int D, bool CAUSAL, int NW, bool BAL = false>
+template <typename T, int D, bool CAUSAL, int NW>
 __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const T* __restrict__ Q, const T* __restrict__ K,
                                                            const T* __restrict__ V, T* __restrict__ O,
                                                            float* __restrict__ LSE, int S, int Hq, int Hkv, long ldq,
@@ -494,14 +515,14 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const T* __restrict__
       const T* Vt = s_cur + TILE;
       auto iter = [&](auto next_c, auto diag_c) {
         constexpr bool NEXT = decltype(next_c)::value, DIAG = decltype(diag_c)::value;
-        // BAL: phase A exponentiates 24 of tile t's 32 scores per lane (all of c0, the first half of
-        // c1) and phase B the last 8 (c1[8..15], only read by the P.V k-step of its second half)
-        // in its first half, so both phases carry about the same VALU per MFMA; otherwise phase A
-        // takes all 32 exponentials and phase B only the row max.
-        constexpr int NEA = BAL ? 24 : 32;
+        // Phase A exponentiates 24 of tile t's 32 scores per lane (all of c0, the first half of c1)
+        // and phase B the last 8 (c1[8..15], only read by the P.V k-step of its second half) in its
+        // first half, so both phases carry about the same VALU per MFMA (B16 S2048 H32 fwd 0.747 ->
+        // 0.734 ms, B1 S8192 H32/8 0.520 -> 0.508 ms against all 32 in phase A).
+        constexpr int NEA = 24;
         constexpr int RA = NKS, EA = NEA / RA;  // phase A: regions / softmax elements per region
         constexpr int RB = 2 * NDB, EB = 32 / RB;
-        constexpr int EBX = BAL ? (32 - NEA) / (RB / 2) : 0;  // phase B exponentials per region
+        constexpr int EBX = (32 - NEA) / (RB / 2);  // phase B exponentials per region
         f32x16 n0 = f32x16{}, n1 = f32x16{};
         float rs = 0.f, mx = -INFINITY;
         auto expo = [&](int e) {  // element e of the 32 scores of tile t
@@ -532,7 +553,6 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const T* __restrict__
           a1 = b1;
           __builtin_amdgcn_sched_barrier(0);
         }
-        if (!BAL) l_i += half_sum(rs);
         V8<T> p[4] = {pack8<T>(c0, 0), pack8<T>(c0, 1), pack8<T>(c1, 0), pack8<T>(c1, 1)};
         if (NEXT && DIAG) mask(n0, n1, (t + 1) * KT);
         // phase B: O^T += V_t^T P_t | row max of tile t+1
@@ -548,14 +568,12 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const T* __restrict__
           const int s0 = 2 * k, s1 = s0 + 1;
           o[s0 % NDB] = mfma(vc[0], p[s0 / NDB], o[s0 % NDB]);
           o[s1 % NDB] = mfma(vc[1], p[s1 / NDB], o[s1 % NDB]);
-          if constexpr (BAL) {
-            if (k < RB / 2) {
+          if (k < RB / 2) {
 #pragma unroll
-              for (int e = 0; e < EBX; ++e) expo(NEA + k * EBX + e);
-              if (k == RB / 2 - 1) {  // P of keys 48..63 complete (first read in region 3 RB / 4)
-                p[3] = pack8<T>(c1, 1);
-                l_i += half_sum(rs);
-              }
+            for (int e = 0; e < EBX; ++e) expo(NEA + k * EBX + e);
+            if (k == RB / 2 - 1) {  // P of keys 48..63 complete (first read in region 3 RB / 4)
+              p[3] = pack8<T>(c1, 1);
+              l_i += half_sum(rs);
             }
           }
           if (NEXT) {
@@ -603,62 +621,6 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const T* __restrict__
 }
 
 // ======================================================================================
-// Backward preprocess (PRA_ATTN_DELTA_PRE=1 only; by default the dQ kernel computes delta itself):
-// delta[b,h,q] = sum_d dO[q,h,d] * O[q,h,d]  (fp32)
-// Block = (b, PRE_QB consecutive queries, all heads): the [PRE_QB, Hq, D] slabs of O and dO are
-// contiguous per token, so the reads stream at full width with 4 rows in flight per lane; the
-// per-row sums are staged in LDS and written out along q (runs of PRE_QB floats per head) instead
-// of one scattered 4-B store per row.
-// ======================================================================================
-constexpr int PRE_QB = 16;
-constexpr int PRE_MAXH = 128;
-template <typename T, int D>
-__global__ __launch_bounds__(256) void bwd_pre_kernel(const T* __restrict__ O, const T* __restrict__ dO,
-                                                      float* __restrict__ delta, int B, int S, int Hq, long ldo,
-                                                      long lddo) {
-  constexpr int LPR = D / 8;     // lanes per row
-  constexpr int RPP = 256 / LPR;  // rows per pass
-  constexpr int U = 4;           // passes in flight
-  __shared__ float red[PRE_QB * (PRE_MAXH + 1)];
-  const int nqb = S / PRE_QB;
-  const int b = blockIdx.x / nqb, q0 = (blockIdx.x % nqb) * PRE_QB;
-  const int rows = PRE_QB * Hq;  // row r = qi * Hq + h
-  const int sub = threadIdx.x % LPR;
-  const long tok0 = (long)b * S + q0;
-  for (int base = threadIdx.x / LPR; base < rows; base += RPP * U) {
-    float a[U][8], c[U][8];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int r = base + u * RPP;
-      if (r < rows) {
-        const long t = tok0 + r / Hq;
-        const int h = r % Hq;
-        load8<T>(O + t * ldo + h * D + sub * 8, a[u]);
-        load8<T>(dO + t * lddo + h * D + sub * 8, c[u]);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) a[u][j] = c[u][j] = 0.f;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      float acc = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc += a[u][j] * c[u][j];
-#pragma unroll
-      for (int off = LPR / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-      const int r = base + u * RPP;
-      if (r < rows && sub == 0) red[(r / Hq) * (PRE_MAXH + 1) + r % Hq] = acc;
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < rows; i += 256) {
-    const int h = i / PRE_QB, qi = i % PRE_QB;
-    delta[((long)b * Hq + h) * S + q0 + qi] = red[qi * (PRE_MAXH + 1) + h];
-  }
-}
-
-// ======================================================================================
 // Backward dK/dV: block = (b, kv head, 32*NW-key tile); wave owns 32 keys. K and V of the block
 // stay resident in LDS (read as MFMA operands, so only the dK/dV accumulators live in registers
 // and the kernel fits 2 waves/SIMD); 32-row Q/dO tiles stream through a single LDS buffer,
@@ -671,14 +633,12 @@ __global__ __launch_bounds__(256) void bwd_pre_kernel(const T* __restrict__ O, c
 // NW = 4 (128 keys, 80 KB, two blocks per CU): the constants arrive as one float per lane and are
 // broadcast with ds_bpermute (no LDS left for them).
 // ======================================================================================
-// WDS: also store dS (bf16/fp16, the exact values the dK MFMAs consume) into dS[b, hq, q, k]
-// ([S, S] per head; only tiles on or below the causal diagonal are written), for bwd_dq_ds_kernel.
-template <typename T, int D, bool CAUSAL, int NW, bool WDS = false>
+template <typename T, int D, bool CAUSAL, int NW>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
     const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V,
     const T* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
     T* __restrict__ dK, T* __restrict__ dV, int S, int Hq, int Hkv, long ldq, long ldk, long ldv,
-    long lddo, long lddk, long lddv, float scale, float scale_log2, int prio, int skv, T* __restrict__ dS = nullptr) {
+    long lddo, long lddk, long lddv, float scale, float scale_log2, int skv, const float2* __restrict__ rtab) {
   constexpr int KB = 32 * NW, QT = 32, NT = NW * 64;
   constexpr int NKS = D / 16, NDB = D / 32;
   constexpr int KVT = KB * D, QDT = QT * D;
@@ -736,9 +696,6 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
     if (ROWC_LDS && wid == 0) rc_next = rc_base[(long)hq * S + q0] * rc_mul;
   };
   if (total > 0) stage_load(0);
-  // one wave per SIMD runs ahead: its MFMA chains win issue, so its softmax VALU overlaps the
-  // partner wave's MFMAs instead of both waves alternating MFMA and VALU phases in lockstep
-  if (prio && NW == 8 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
 
   for (int it = 0; it < total; ++it) {
     const int hq = hk * nrep + it / nqt;
@@ -798,18 +755,6 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
         }
       }
       const V8<T> p0 = pack8<T>(s, 0), p1 = pack8<T>(s, 1), d0 = pack8<T>(dp, 0), d1 = pack8<T>(dp, 1);
-      if constexpr (WDS) {
-        // column krow of rows q0 + crow(r, h2) of this head's [S, S] dS (lanes of a half-wave write
-        // 64 B): buffer stores with the lane part in one VGPR offset and the row in the scalar offset
-        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(dS + (long)__builtin_amdgcn_readfirstlane(b * Hq + hq) * S * S), (short)0,
-            __builtin_amdgcn_readfirstlane(S * S * 2), 0x00020000);
-        const int voff = (4 * h2 * S + krow) * 2;
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (T)dp[r]), rsrc, voff,
-                                                __builtin_amdgcn_readfirstlane((q0 + crow(r, 0)) * S * 2), 0);
-      }
       V8<T> ot = lo.tr(Ds, 0, 0), qt = lo.tr(Qs, 0, 0);
 #pragma unroll
       for (int st = 0; st < 2 * NDB; ++st) {
@@ -827,7 +772,9 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
     __syncthreads();
   }
 
-  store_rows16<T, NDB>(dkt, scale, dK + ((long)b * S + krow) * lddk + hk * D, true, h2);
+  // rtab: inverse RoPE on dK (table rows = positions; padded rows >= skv are discarded, clamp them)
+  store_rows16<T, NDB>(dkt, scale, dK + ((long)b * S + krow) * lddk + hk * D, true, h2,
+                       rtab ? rtab + (long)min(krow, skv - 1) * (D / 2) : nullptr);
   store_rows16<T, NDB>(dvt, 1.f, dV + ((long)b * S + krow) * lddv + hk * D, true, h2);
 }
 
@@ -847,7 +794,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
     const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V,
     const T* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
     T* __restrict__ dK, T* __restrict__ dV, int S, int Hq, int Hkv, long ldq, long ldk, long ldv,
-    long lddo, long lddk, long lddv, float scale, float scale_log2, int skv) {
+    long lddo, long lddk, long lddv, float scale, float scale_log2, int skv, const float2* __restrict__ rtab) {
   constexpr int NW = 4, KB = 32 * NW, QS = 64;
   constexpr int NKS = D / 16, NDB = D / 32;
   constexpr int KVT = KB * D, QDT = QS * D;
@@ -997,7 +944,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
   }
 
   const int krow = kw + l32;
-  store_rows16<T, NDB>(dkt, scale, dK + ((long)b * S + krow) * lddk + hk * D, true, h2);
+  // rtab: inverse RoPE on dK (table rows = positions; padded rows >= skv are discarded, clamp them)
+  store_rows16<T, NDB>(dkt, scale, dK + ((long)b * S + krow) * lddk + hk * D, true, h2,
+                       rtab ? rtab + (long)min(krow, skv - 1) * (D / 2) : nullptr);
   store_rows16<T, NDB>(dvt, 1.f, dV + ((long)b * S + krow) * lddv + hk * D, true, h2);
 }
 
@@ -1015,7 +964,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
     const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V,
     const T* __restrict__ dO, const T* __restrict__ O, const float* __restrict__ LSE, float* __restrict__ Delta,
     T* __restrict__ dQ, int S, int Hq, int Hkv, long ldq, long ldk, long ldv, long lddo, long ldo, long lddq,
-    float scale, float scale_log2, int prio, int skv, int delta_in) {
+    float scale, float scale_log2, int skv, const float2* __restrict__ rtab) {
   constexpr int KT = 64, QT = 32 * NW;
   constexpr int NKS = D / 16, NDB = D / 32, TILE = KT * D;
   // K0 V0 | K1 V1: one __shared__ object per buffer, so the reads of one buffer do not wait
@@ -1060,9 +1009,6 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
   {
     float part = 0.f;
     if (qrow < S) lse2 = LSE[((long)b * Hq + hq) * S + qrow] * 1.4426950408889634f;
-    if (delta_in) {
-      if (qrow < S) dl = Delta[((long)b * Hq + hq) * S + qrow];
-    } else {
     if (qrow < S) {
       const T* Orow = O + ((long)b * S + qrow) * ldo + hq * D + 8 * h2;
 #pragma unroll
@@ -1074,7 +1020,6 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
     }
     dl = half_sum(part);  // all 64 lanes (permlane32 swap)
     if (qrow < S && h2 == 0) Delta[((long)b * Hq + hq) * S + qrow] = dl;
-    }
   }
 
   f32x16 dqt[NDB];
@@ -1090,8 +1035,6 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
   gk.issue(Kb, kvb0);
   gv.issue(Vb, kvb0 + TILE);
   __syncthreads();
-  if (prio && NW == 8 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
-
   auto body = [&](auto cc, int kt) {
     constexpr int CUR = decltype(cc)::value;
     T* const cur_b = CUR ? kvb1 : kvb0;
@@ -1210,94 +1153,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
     if (kt + 1 < nkt) body(IC<1>{}, kt + 1);
   }
 
-  store_rows16<T, NDB>(dqt, scale, dQ + ((long)b * S + qrow) * lddq + hq * D, qrow < S, h2);
-}
-
-// ======================================================================================
-// Backward dQ from a materialized dS (causal, after bwd_dkdv_kernel<..., WDS>): dQ^T = K^T dS^T.
-// Block = (b, q head, 32 NW queries), wave = 32 queries; 64-key K tiles by LDS-DMA (double buffer,
-// one __shared__ object per buffer), dS fragments loaded straight into registers one tile ahead.
-// One GEMM per key tile instead of the three of bwd_dq_kernel (S and dP are not recomputed);
-// keys past a wave's last query are masked on its diagonal tile (dS is not written there).
-// ======================================================================================
-template <typename T, int D, int NW>
-__global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_ds_kernel(const T* __restrict__ K,
-                                                                    const T* __restrict__ dS, T* __restrict__ dQ,
-                                                                    int S, int Hq, int Hkv, long ldk, long lddq,
-                                                                    float scale) {
-  constexpr int KT = 64, QT = 32 * NW;
-  constexpr int NDB = D / 32, TILE = KT * D;
-  __shared__ __attribute__((aligned(16))) T kb0[TILE];
-  __shared__ __attribute__((aligned(16))) T kb1[TILE];
-
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h2 = lane >> 5, l32 = lane & 31;
-  const int nqt = S / QT;
-  const int BH = gridDim.x / nqt;
-  const int qt = nqt - 1 - (int)(blockIdx.x / BH);  // heavy (late) query tiles first
-  const int bh = blockIdx.x % BH;
-  const int hq = bh % Hq, b = bh / Hq;
-  const int hk = hq / (Hq / Hkv);
-  const int q0 = qt * QT, qw = q0 + wid * 32;
-  const int qrow = qw + l32;
-
-  const T* Kb = K + (long)b * S * ldk + hk * D;
-  const T* dsr = dS + ((long)(b * Hq + hq) * S + qrow) * S + 4 * h2;  // this lane's dS row
-
-  LaneOff<T, D> lo;
-  lo.init(lane);
-  f32x16 dqt[NDB];
-#pragma unroll
-  for (int i = 0; i < NDB; ++i) dqt[i] = f32x16{};
-
-  const int nkt = (q0 + QT) / KT;  // causal: key tiles up to the block's last query
-  const int lastw = (qw + 31) / KT;  // this wave's last (diagonal) tile
-  // B operand of k-step k4 (keys 16 k4 ..): the k order of lo.tr's transposed A fragment, i.e.
-  // keys 16 k4 + {4 h2 .. 4 h2 + 3} then 16 k4 + 8 + {4 h2 .. +3}
-  auto load_ds = [&](int kt, V8<T> (&f)[4]) {
-#pragma unroll
-    for (int k4 = 0; k4 < 4; ++k4) {
-      const uint2 a = *reinterpret_cast<const uint2*>(dsr + kt * KT + 16 * k4);
-      const uint2 c = *reinterpret_cast<const uint2*>(dsr + kt * KT + 16 * k4 + 8);
-      f[k4] = __builtin_bit_cast(V8<T>, make_uint4(a.x, a.y, c.x, c.y));
-    }
-  };
-
-  GStage<T, D, KT, NW> gk;
-  gk.init(ldk);
-  gk.issue(Kb, kb0);
-  V8<T> fc[4], fn[4];
-  if (0 <= lastw) load_ds(0, fc);
-  __syncthreads();
-
-  auto body = [&](auto cc, int kt) {
-    constexpr int CUR = decltype(cc)::value;
-    const T* Kt = CUR ? kb1 : kb0;
-    if (kt + 1 < nkt) gk.issue(Kb + (long)(kt + 1) * KT * ldk, CUR ? kb0 : kb1);
-    if (kt <= lastw) {
-      if (kt + 1 <= lastw) load_ds(kt + 1, fn);
-      if (kt == lastw) {  // diagonal tile: dS of keys past this lane's query was never written
-#pragma unroll
-        for (int k4 = 0; k4 < 4; ++k4)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int key = kt * KT + 16 * k4 + (j < 4 ? 4 * h2 + j : 8 + 4 * h2 + j - 4);
-            if (key > qrow) fc[k4][j] = (T)0.f;
-          }
-      }
-#pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4)
-#pragma unroll
-        for (int db = 0; db < NDB; ++db) dqt[db] = mfma(lo.tr(Kt, 16 * k4, db), fc[k4], dqt[db]);
-#pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4) fc[k4] = fn[k4];
-    }
-    __syncthreads();  // the next K tile landed (vmcnt(0)); this buffer is free
-  };
-  for (int kt = 0; kt < nkt; kt += 2) {
-    body(IC<0>{}, kt);
-    if (kt + 1 < nkt) body(IC<1>{}, kt + 1);
-  }
-  store_rows16<T, NDB>(dqt, scale, dQ + ((long)b * S + qrow) * lddq + hq * D, true, h2);
+  store_rows16<T, NDB>(dqt, scale, dQ + ((long)b * S + qrow) * lddq + hq * D, qrow < S, h2,
+                       rtab ? rtab + (long)min(qrow, skv - 1) * (D / 2) : nullptr);
 }
 
 }  // namespace attn
@@ -1306,6 +1163,25 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_ds_kernel(const T* __r
 using namespace pra::attn;
 
 namespace {
+
+// Kernel selection knobs. Set through pra_attn_set_options (pyrecover_amd.ops.fused reads the
+// PYRECOVER_ATTN_* environment once; tests switch them per case); the launchers read no environment.
+struct AttnOptions {
+  // forward: -1 = by shape (pipelined fwd_p_kernel for causal, fwd_kernel for full attention),
+  // 0 = fwd_kernel, 1 = fwd_p_kernel. The pipelined kernel's non-causal instantiation spills at
+  // D = 128, and padded non-causal keys (skv < S) need fwd_kernel's key bound.
+  // (B8 S2048 H32: 0.460 -> 0.422 ms; S8192 H32/8: 0.654 -> 0.615 ms with the pipelined kernel.)
+  int fwd_pipe = -1;
+  // Rescale threshold of the pipelined forward (cdna guide T13), log2 units: O and l are rescaled
+  // only when some row's max grows by more than thr, so P stays below 2^thr (fp32 accumulators;
+  // bf16 P keeps its relative precision). 0 = exact rescale at every growth.
+  float fwd_thr = 8.f;
+  // dK/dV: -1 = by shape (dkdv_use_p2), 0 = two-wave bwd_dkdv_kernel, 1 = pipelined bwd_dkdv_p2_kernel
+  int dkdv_impl = -1;
+  // dQ: -1/1 = region-pipelined bwd_dq_kernel<PIPE>, 0 = plain (padded non-causal keys: always plain)
+  int dq_pipe = -1;
+};
+AttnOptions g_attn_opts;
 
 // All tensors bf16 or fp16 (T), layout [B, S, H, D] with token stride ld* (elements); LSE/Delta fp32 [B, Hq, S].
 template <typename T>
@@ -1318,157 +1194,59 @@ hipError_t attn_fwd_t(const void* q, const void* k, const void* v, void* o, floa
   const int nqt = (S + 32 * NW - 1) / (32 * NW);
   dim3 grid(nqt * Hq * B), block(NW * 64);
   const float sl2 = scale * 1.4426950408889634f;
-  // PRA_FWD_PIPE (read per call; tests switch it): the pipelined kernel is the default for causal
-  // attention (B8 S2048 H32: 0.460 -> 0.422 ms; S8192 H32/8: 0.654 -> 0.615 ms). Its non-causal
-  // instantiation spills at D = 128, so full attention stays on fwd_kernel.
-  const char* fp = getenv("PRA_FWD_PIPE");
-  // non-causal with padded keys (skv < S) needs fwd_kernel's key bound
-  const bool pipe = (causal || skv >= S) && (fp ? atoi(fp) != 0 : (causal != 0));
-  // Rescale threshold of the pipelined kernels (cdna guide T13), log2 units: O and l are rescaled
-  // only when some row's max grows by more than thr, so P stays below 2^thr (fp32 accumulators;
-  // bf16 P keeps its relative precision). With 32 rows per wave a rescale fires whenever ANY row's
-  // max grows, which on causal random data is most early tiles. PRA_FWD_THR (per call), default 8;
-  // 0 = exact rescale at every growth.
-  const char* ft = getenv("PRA_FWD_THR");
-  const float thr = ft ? (float)atof(ft) : 8.f;
-  // PRA_FWD_BAL (read per call, default 1): exponentials split between the two phases of the
-  // pipelined kernel (B16 S2048 H32 fwd 0.747 -> 0.734 ms, B1 S8192 H32/8 0.520 -> 0.508 ms)
-  const char* fb = getenv("PRA_FWD_BAL");
-  const bool bal = fb ? atoi(fb) != 0 : true;
+  const AttnOptions& op = g_attn_opts;
+  const bool pipe = (causal || skv >= S) && (op.fwd_pipe >= 0 ? op.fwd_pipe != 0 : (causal != 0));
+  const float thr = op.fwd_thr;
 #define LAUNCH(DD, CC)                                                                                        \
-  if (pipe && bal)                                                                                            \
-    hipLaunchKernelGGL((fwd_p_kernel<T, DD, CC, NW, true>), grid, block, 0, st, (const T*)q, (const T*)k,   \
-                       (const T*)v, (T*)o, lse, S, Hq, Hkv, ldq, ldk, ldv, ldo, sl2, thr);                  \
-  else if (pipe)                                                                                              \
+  if (pipe)                                                                                                   \
     hipLaunchKernelGGL((fwd_p_kernel<T, DD, CC, NW>), grid, block, 0, st, (const T*)q, (const T*)k,         \
                        (const T*)v, (T*)o, lse, S, Hq, Hkv, ldq, ldk, ldv, ldo, sl2, thr);                  \
   else                                                                                                        \
-  hipLaunchKernelGGL((fwd_kernel<T, DD, CC, NW>), grid, block, 0, st, (const T*)q, (const T*)k,             \
-                     (const T*)v, (T*)o, lse, S, Hq, Hkv, ldq, ldk, ldv, ldo, sl2, skv)
+    hipLaunchKernelGGL((fwd_kernel<T, DD, CC, NW>), grid, block, 0, st, (const T*)q, (const T*)k,           \
+                       (const T*)v, (T*)o, lse, S, Hq, Hkv, ldq, ldk, ldv, ldo, sl2, skv)
   if (D == 128) { if (causal) LAUNCH(128, true); else LAUNCH(128, false); }
   else { if (causal) LAUNCH(64, true); else LAUNCH(64, false); }
 #undef LAUNCH
   return hipGetLastError();
 }
 
-// Kernel choices of the backward, shared by the launcher and pra_attn_bwd_ds_bytes.
-// dK/dV: D = 64: 64 KB of LDS and <= 256 VGPRs, so two pipelined one-wave blocks share a CU and hide
-// each other's prologue (B16 S2048 H16: 0.74 -> 0.68 ms bwd). At D = 128 the pipelined kernel wins
-// only while the two-wave kernel's grid ((S/256) Hkv B blocks, one per CU) is at most one round of
-// the chip's 256 CUs, where its causal work imbalance is exposed: S 8192 GQA 32/8 bwd B1
+// dK/dV kernel choice. D = 64: 64 KB of LDS and <= 256 VGPRs, so two pipelined one-wave blocks share
+// a CU and hide each other's prologue (B16 S2048 H16: 0.74 -> 0.68 ms bwd). At D = 128 the pipelined
+// kernel wins only while the two-wave kernel's grid ((S/256) Hkv B blocks, one per CU) is at most one
+// round of the chip's 256 CUs, where its causal work imbalance is exposed: S 8192 GQA 32/8 bwd B1
 // 2.56 -> 1.98 ms with p2, but B4 7.30 (two-wave) vs 7.89 ms (p2) (profiles/attn_dkdv_select_r2.log).
-// PRA_DKDV_IMPL: 1 = pipelined, 0 = two-wave, unset = by shape (read per call; tests switch it).
 static bool dkdv_use_p2(int B, int S, int Hq, int Hkv, int D) {
-  const char* impl_s = getenv("PRA_DKDV_IMPL");
-  const int impl_env = impl_s ? atoi(impl_s) : -1;
+  const int impl = g_attn_opts.dkdv_impl;
   const long grid2 = (long)(S / 256) * Hkv * B;
-  return impl_env == 1 || (impl_env < 0 && (D == 64 || ((long)(Hq / Hkv) * S >= 8192 && grid2 <= 256)));
-}
-static int dkdv_nw_env() {
-  static const int v = [] {
-    const char* e = getenv("PRA_DKDV_NW");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-// dS-materializing path (causal): dK/dV (two-wave, 8 waves) also writes dS, then a one-GEMM dQ
-// kernel reads it -- S and dP are computed once instead of in both kernels. Needs a [B, Hq, S, S]
-// 16-bit workspace (capped at 8 GiB). PRA_ATTN_DS (read per call): 0 = off, 1 = on.
-static size_t ds_path_bytes(int B, int S, int Hq, int Hkv, int D, int causal) {
-  const char* e = getenv("PRA_ATTN_DS");
-  if (!(e ? atoi(e) != 0 : false)) return 0;
-  if (!causal || D != 128 || S % 256 || Hq > PRE_MAXH) return 0;
-  if (dkdv_use_p2(B, S, Hq, Hkv, D) || dkdv_nw_env() == 4) return 0;
-  const size_t bytes = (size_t)B * Hq * S * S * 2;
-  return bytes <= (8ull << 30) ? bytes : 0;
+  return impl == 1 || (impl < 0 && (D == 64 || ((long)(Hq / Hkv) * S >= 8192 && grid2 <= 256)));
 }
 
 template <typename T>
 hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o, const void* dout,
                         const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int S, int Hq, int Hkv,
                         int D, long ldq, long ldk, long ldv, long ldo, long lddo, long lddq, long lddk, long lddv,
-                        float scale, int causal, int skv, void* ds_ws, size_t ds_bytes, hipStream_t st) {
+                        float scale, int causal, int skv, const float* rope_tab, hipStream_t st) {
   if (S % 128 || (D != 64 && D != 128) || Hq % Hkv) return hipErrorInvalidValue;
+  const float2* rt = reinterpret_cast<const float2*>(rope_tab);
   if (ldq % 8 || ldk % 8 || ldv % 8 || ldo % 8 || lddo % 8 || lddq % 8 || lddk % 8 || lddv % 8)
     return hipErrorInvalidValue;
   const float sl2 = scale * 1.4426950408889634f;
-  static const int bwd_prio = [] {
-    const char* e = getenv("PRA_ATTN_BWD_PRIO");
-    return e ? atoi(e) : 0;
-  }();
-  if (ds_ws != nullptr && ds_bytes >= ds_path_bytes(B, S, Hq, Hkv, D, causal) &&
-      ds_path_bytes(B, S, Hq, Hkv, D, causal) > 0) {
-    // delta = rowsum(dO * O) first (the dK/dV kernel reads it), then dK/dV + dS, then dQ from dS
-    hipLaunchKernelGGL((bwd_pre_kernel<T, 128>), dim3(B * (S / PRE_QB)), dim3(256), 0, st, (const T*)o,
-                       (const T*)dout, delta, B, S, Hq, ldo, lddo);
-    hipLaunchKernelGGL((bwd_dkdv_kernel<T, 128, true, 8, true>), dim3((S / 256) * Hkv * B), dim3(512), 0, st,
-                       (const T*)q, (const T*)k, (const T*)v, (const T*)dout, lse, (const float*)delta, (T*)dk,
-                       (T*)dv, S, Hq, Hkv, ldq, ldk, ldv, lddo, lddk, lddv, scale, sl2, bwd_prio, skv, (T*)ds_ws);
-    hipLaunchKernelGGL((bwd_dq_ds_kernel<T, 128, 8>), dim3((S / 256) * Hq * B), dim3(512), 0, st, (const T*)k,
-                       (const T*)ds_ws, (T*)dq, S, Hq, Hkv, ldk, lddq, scale);
-    return hipGetLastError();
-  }
+  // 8-wave (256-row) blocks; S % 256 != 0 (S % 128 == 0) takes the 4-wave instantiations
+  const int nw = S % 256 ? 4 : 8;
   // dQ first: it also computes delta = rowsum(dO * O), which the dK/dV kernel reads
-  // (PRA_ATTN_DELTA_PRE=1: a separate preprocess kernel computes it, read per call for A/B tests)
-  const char* dpre_s = getenv("PRA_ATTN_DELTA_PRE");
-  const int delta_pre = dpre_s ? atoi(dpre_s) : 0;
-  if (delta_pre) {
-    if (Hq > PRE_MAXH) return hipErrorInvalidValue;
-    const int grid = B * (S / PRE_QB);
-    if (D == 128)
-      hipLaunchKernelGGL((bwd_pre_kernel<T, 128>), dim3(grid), dim3(256), 0, st, (const T*)o, (const T*)dout, delta, B,
-                         S, Hq, ldo, lddo);
-    else
-      hipLaunchKernelGGL((bwd_pre_kernel<T, 64>), dim3(grid), dim3(256), 0, st, (const T*)o, (const T*)dout, delta, B,
-                         S, Hq, ldo, lddo);
-  }
   {
-    static const int dq_env = [] {
-      const char* e = getenv("PRA_DQ_NW");
-      return e ? atoi(e) : 0;
-    }();
-    const int nwq = (dq_env == 4 || S % 256) ? 4 : 8;
-    dim3 grid(((S + 32 * nwq - 1) / (32 * nwq)) * Hq * B);
-    const char* pipe_s = getenv("PRA_DQ_PIPE");  // read per call (tests switch it)
+    dim3 grid((S / (32 * nw)) * Hq * B);
     // the pipelined kernel has no key bound: padded non-causal sequences take the plain one
-    const bool pipe = (causal || skv >= S) && (pipe_s ? atoi(pipe_s) != 0 : true);
+    const bool pipe = (causal || skv >= S) && g_attn_opts.dq_pipe != 0;
 #define LAUNCH(DD, CC, NWW)                                                                                     \
   if (pipe)                                                                                                     \
-  hipLaunchKernelGGL((bwd_dq_kernel<T, DD, CC, NWW, true>), grid, dim3(NWW * 64), 0, st, (const T*)q,         \
-                     (const T*)k, (const T*)v, (const T*)dout, (const T*)o, lse, delta, (T*)dq, S, \
-                     Hq, Hkv, ldq, ldk, ldv, lddo, ldo, lddq, scale, sl2, bwd_prio, skv, delta_pre);                                            \
+    hipLaunchKernelGGL((bwd_dq_kernel<T, DD, CC, NWW, true>), grid, dim3(NWW * 64), 0, st, (const T*)q,       \
+                       (const T*)k, (const T*)v, (const T*)dout, (const T*)o, lse, delta, (T*)dq, S, Hq, Hkv,  \
+                       ldq, ldk, ldv, lddo, ldo, lddq, scale, sl2, skv, rt);                                        \
   else                                                                                                          \
-  hipLaunchKernelGGL((bwd_dq_kernel<T, DD, CC, NWW>), grid, dim3(NWW * 64), 0, st, (const T*)q,               \
-                     (const T*)k, (const T*)v, (const T*)dout, (const T*)o, lse, delta, (T*)dq, S, \
-                     Hq, Hkv, ldq, ldk, ldv, lddo, ldo, lddq, scale, sl2, bwd_prio, skv, delta_pre)
-    if (nwq == 8) {
-      if (D == 128) { if (causal) LAUNCH(128, true, 8); else LAUNCH(128, false, 8); }
-      else { if (causal) LAUNCH(64, true, 8); else LAUNCH(64, false, 8); }
-    } else {
-      if (D == 128) { if (causal) LAUNCH(128, true, 4); else LAUNCH(128, false, 4); }
-      else { if (causal) LAUNCH(64, true, 4); else LAUNCH(64, false, 4); }
-    }
-#undef LAUNCH
-  }
-  {
-    const int nw_env = dkdv_nw_env();
-    const int nw = (nw_env == 4 || S % 256) ? 4 : 8;
-    const bool p2 = dkdv_use_p2(B, S, Hq, Hkv, D);
-    if (p2 && nw_env == 0) {
-      dim3 g1((S / 128) * Hkv * B);
-#define LAUNCH1(DD, CC)                                                                                       \
-  hipLaunchKernelGGL((bwd_dkdv_p2_kernel<T, DD, CC>), g1, dim3(256), 0, st, (const T*)q, (const T*)k,    \
-                     (const T*)v, (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Hq, Hkv, ldq, \
-                     ldk, ldv, lddo, lddk, lddv, scale, sl2, skv)
-      if (D == 128) { if (causal) LAUNCH1(128, true); else LAUNCH1(128, false); }
-      else { if (causal) LAUNCH1(64, true); else LAUNCH1(64, false); }
-#undef LAUNCH1
-    } else {
-    dim3 grid((S / (32 * nw)) * Hkv * B);
-#define LAUNCH(DD, CC, NWW)                                                                                     \
-  hipLaunchKernelGGL((bwd_dkdv_kernel<T, DD, CC, NWW>), grid, dim3(NWW * 64), 0, st, (const T*)q,             \
-                     (const T*)k, (const T*)v, (const T*)dout, lse, delta, (T*)dk, (T*)dv, \
-                     S, Hq, Hkv, ldq, ldk, ldv, lddo, lddk, lddv, scale, sl2, bwd_prio, skv)
+    hipLaunchKernelGGL((bwd_dq_kernel<T, DD, CC, NWW>), grid, dim3(NWW * 64), 0, st, (const T*)q,             \
+                       (const T*)k, (const T*)v, (const T*)dout, (const T*)o, lse, delta, (T*)dq, S, Hq, Hkv,  \
+                       ldq, ldk, ldv, lddo, ldo, lddq, scale, sl2, skv, rt)
     if (nw == 8) {
       if (D == 128) { if (causal) LAUNCH(128, true, 8); else LAUNCH(128, false, 8); }
       else { if (causal) LAUNCH(64, true, 8); else LAUNCH(64, false, 8); }
@@ -1477,7 +1255,30 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
       else { if (causal) LAUNCH(64, true, 4); else LAUNCH(64, false, 4); }
     }
 #undef LAUNCH
+  }
+  if (dkdv_use_p2(B, S, Hq, Hkv, D)) {
+    dim3 g1((S / 128) * Hkv * B);
+#define LAUNCH1(DD, CC)                                                                                       \
+  hipLaunchKernelGGL((bwd_dkdv_p2_kernel<T, DD, CC>), g1, dim3(256), 0, st, (const T*)q, (const T*)k,        \
+                     (const T*)v, (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Hq, Hkv, ldq, ldk, ldv, lddo, \
+                     lddk, lddv, scale, sl2, skv, rt)
+    if (D == 128) { if (causal) LAUNCH1(128, true); else LAUNCH1(128, false); }
+    else { if (causal) LAUNCH1(64, true); else LAUNCH1(64, false); }
+#undef LAUNCH1
+  } else {
+    dim3 grid((S / (32 * nw)) * Hkv * B);
+#define LAUNCH(DD, CC, NWW)                                                                                     \
+  hipLaunchKernelGGL((bwd_dkdv_kernel<T, DD, CC, NWW>), grid, dim3(NWW * 64), 0, st, (const T*)q, (const T*)k, \
+                     (const T*)v, (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Hq, Hkv, ldq, ldk, ldv, lddo,  \
+                     lddk, lddv, scale, sl2, skv, rt)
+    if (nw == 8) {
+      if (D == 128) { if (causal) LAUNCH(128, true, 8); else LAUNCH(128, false, 8); }
+      else { if (causal) LAUNCH(64, true, 8); else LAUNCH(64, false, 8); }
+    } else {
+      if (D == 128) { if (causal) LAUNCH(128, true, 4); else LAUNCH(128, false, 4); }
+      else { if (causal) LAUNCH(64, true, 4); else LAUNCH(64, false, 4); }
     }
+#undef LAUNCH
   }
   return hipGetLastError();
 }
@@ -1500,21 +1301,23 @@ hipError_t pra_attn_fwd(int dtype, const void* q, const void* k, const void* v, 
 hipError_t pra_attn_bwd(int dtype, const void* q, const void* k, const void* v, const void* o, const void* dout,
                         const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int S, int Hq, int Hkv,
                         int D, long ldq, long ldk, long ldv, long ldo, long lddo, long lddq, long lddk, long lddv,
-                        float scale, int causal, int skv, void* ds_ws, size_t ds_bytes, hipStream_t st) {
+                        float scale, int causal, int skv, const float* rope_tab, hipStream_t st) {
   if (skv <= 0 || skv > S) return hipErrorInvalidValue;
   if (dtype == pra::kBF16)
     return attn_bwd_t<__bf16>(q, k, v, o, dout, lse, delta, dq, dk, dv, B, S, Hq, Hkv, D, ldq, ldk, ldv, ldo, lddo,
-                              lddq, lddk, lddv, scale, causal, skv, ds_ws, ds_bytes, st);
+                              lddq, lddk, lddv, scale, causal, skv, rope_tab, st);
   if (dtype == pra::kF16)
     return attn_bwd_t<_Float16>(q, k, v, o, dout, lse, delta, dq, dk, dv, B, S, Hq, Hkv, D, ldq, ldk, ldv, ldo, lddo,
-                                lddq, lddk, lddv, scale, causal, skv, ds_ws, ds_bytes, st);
+                                lddq, lddk, lddv, scale, causal, skv, rope_tab, st);
   return hipErrorInvalidValue;
 }
 
-// Workspace bytes the backward would use for the dS-materializing path (0: the path is off for
-// this shape / setting; the caller then passes no workspace).
-size_t pra_attn_bwd_ds_bytes(int B, int S, int Hq, int Hkv, int D, int causal) {
-  return ds_path_bytes(B, S, Hq, Hkv, D, causal);
+// Kernel selection (see AttnOptions); not thread-safe against concurrent launches (set between steps).
+void pra_attn_set_options(int fwd_pipe, float fwd_thr, int dkdv_impl, int dq_pipe) {
+  g_attn_opts.fwd_pipe = fwd_pipe;
+  g_attn_opts.fwd_thr = fwd_thr;
+  g_attn_opts.dkdv_impl = dkdv_impl;
+  g_attn_opts.dq_pipe = dq_pipe;
 }
 
 }  // extern "C"

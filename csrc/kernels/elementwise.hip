@@ -108,6 +108,59 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const T* __restrict__ d
   }
 }
 
+// Same op with every load of a lane issued before its first store: dg/du alias g/u (in-place
+// backward), so in the grid-stride loop above the compiler may not move a row's loads above an
+// earlier row's stores and each lane has only 3 x 16 B in flight. Block = 16 R tokens x 128 columns
+// (2-D grid: no 64-bit index division); lane = one 16-B column chunk of tokens r, r + 16, ...
+template <typename T>
+struct Raw8 {  // 8 packed elements (16 B for 16-bit types, 32 B for fp32) held while loads are in flight
+  uint4 w[sizeof(T) / 2];
+};
+template <typename T>
+__device__ __forceinline__ Raw8<T> ld_raw8(const T* p) {
+  Raw8<T> r;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 2); ++i) r.w[i] = reinterpret_cast<const uint4*>(p)[i];
+  return r;
+}
+
+template <typename T, int R>
+__global__ __launch_bounds__(256) void swiglu_bwd_tile_kernel(const T* dy, const T* g, const T* u, T* dg, T* du,
+                                                              long ntok, int F, int ldg, int ldu, int lddy) {
+  const int col = blockIdx.x * 128 + (threadIdx.x & 15) * 8;
+  if (col >= F) return;
+  const long t0 = (long)blockIdx.y * (16 * R) + (threadIdx.x >> 4);
+  Raw8<T> G[R], U[R], DY[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const long t = t0 + 16 * i;
+    if (t < ntok) {
+      G[i] = ld_raw8(g + t * ldg + col);
+      U[i] = ld_raw8(u + t * ldu + col);
+      DY[i] = ld_raw8(dy + t * lddy + col);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const long t = t0 + 16 * i;
+    if (t >= ntok) continue;
+    float gv[8], uv[8], dv[8], og[8], ou[8];
+    load8<T>(reinterpret_cast<const T*>(&G[i]), gv);
+    load8<T>(reinterpret_cast<const T*>(&U[i]), uv);
+    load8<T>(reinterpret_cast<const T*>(&DY[i]), dv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {  // identical math / rounding to swiglu_bwd_kernel
+      const float sg = 1.f / (1.f + __expf(-gv[j]));
+      const float a = rnd<T>(gv[j] * sg);
+      const float da = rnd<T>(dv[j] * uv[j]);
+      ou[j] = dv[j] * a;
+      og[j] = da * sg * (1.f + gv[j] * (1.f - sg));
+    }
+    store8<T>(dg + t * ldg + col, og);
+    store8<T>(du + t * ldu + col, ou);
+  }
+}
+
 // ----------------------------------------------------------------------------------------
 // Embedding gather: out[t] = W[ids[t]]; one wave per token.
 template <typename T>
@@ -156,41 +209,13 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const int64_t* __restric
 }
 
 // ---------------------------------------------------------------------------------------
-// 2-D transpose of a 16-bit [R, C] matrix into [C, R] (64x64 tiles through LDS, 16-B loads and
-// stores on both sides). Used to hand hipBLASLt the weight-gradient GEMM in its fast K-contiguous
-// ("TN") layout: dW = dY^T X computed as dYt (Xt)^T with dYt = [out, T], Xt = [in, T].
-// Requires R % 64 == 0, C % 64 == 0, 16-B aligned rows (host-checked).
-template <typename T>
-__global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ src, T* __restrict__ dst, long ld_src,
-                                                        long ld_dst) {
-  __shared__ __attribute__((aligned(16))) uint16_t tile[64][72];  // +8 pad: 16-B rows, fewer conflicts
-  const long r0 = (long)blockIdx.y * 64, c0 = (long)blockIdx.x * 64;
-  const int t = threadIdx.x;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int idx = t + 256 * i, r = idx >> 3, ch = idx & 7;
-    *reinterpret_cast<uint4*>(&tile[r][ch * 8]) =
-        *reinterpret_cast<const uint4*>(src + (r0 + r) * ld_src + c0 + ch * 8);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int idx = t + 256 * i, rg = idx & 7, c = idx >> 3;  // 8 lanes write one 128-B output row piece
-    uint32_t w[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      w[j] = (uint32_t)tile[rg * 8 + 2 * j][c] | ((uint32_t)tile[rg * 8 + 2 * j + 1][c] << 16);
-    *reinterpret_cast<uint4*>(dst + (c0 + c) * ld_dst + r0 + rg * 8) = make_uint4(w[0], w[1], w[2], w[3]);
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// Register transpose (default): one wave moves a 64x64 tile with no LDS and no barrier. Lane
+// 2-D transpose of a 16-bit [R, C] matrix into [C, R] (R, C multiples of 64, 16-B aligned rows;
+// host-checked): one wave moves a 64x64 tile with no LDS and no barrier. Lane
 // (g = lane & 7, ch = lane >> 3) loads the 8x8 sub-block rows 8g..8g+7, cols 8ch..8ch+7 as
 // eight 16-B loads (each instruction: 8 rows x 128 contiguous bytes), transposes it in VGPRs
 // with 32 v_perm_b32, and writes eight 16-B stores (each instruction: 8 output rows x 128 B).
-// 128 B in flight per lane and no LDS bank conflicts (the LDS kernel above reads its tile
-// column-wise with 8-way conflicts, which caps it near HBM rate even in isolation).
+// 128 B in flight per lane and no LDS bank conflicts (an LDS-tiled version read its tile
+// column-wise with 8-way conflicts, which capped it near HBM rate even in isolation).
 __device__ __forceinline__ void transpose8x8_b16(const uint4 (&in)[8], uint4 (&out)[8]) {
   const uint32_t* a = reinterpret_cast<const uint32_t*>(in);
   uint32_t* o = reinterpret_cast<uint32_t*>(out);
@@ -244,14 +269,6 @@ __device__ __forceinline__ void store_tile_t(uint16_t (*tile)[72], uint16_t* dst
 __device__ __forceinline__ int swz(int r, int ch) { return ch ^ ((r >> 3) & 7); }
 
 template <typename T>
-__device__ __forceinline__ void put8(uint16_t* row, const float* v) {
-  T tmp[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) tmp[j] = from_f<T>(v[j]);
-  *reinterpret_cast<uint4*>(row) = *reinterpret_cast<const uint4*>(tmp);
-}
-
-template <typename T>
 __device__ __forceinline__ void unpack8(const uint4& w, float (&o)[8]) {
   const T* e = reinterpret_cast<const T*>(&w);
 #pragma unroll
@@ -266,69 +283,11 @@ __device__ __forceinline__ uint4 pack8(const float (&v)[8]) {
   return *reinterpret_cast<const uint4*>(tmp);
 }
 
-// swiglu_fwd_t: a = silu(g) * u (row-major, for the W2 forward GEMM) and aT = a^T (K-contiguous
-// operand of the W2 weight-gradient GEMM, kept for the backward instead of a).
-template <typename T>
-__global__ __launch_bounds__(256) void swiglu_fwd_t_kernel(const T* __restrict__ gu, T* __restrict__ a,
-                                                           T* __restrict__ aT, int F, int ldgu, int lda, long ntok) {
-  __shared__ __attribute__((aligned(16))) uint16_t ta[64][72];
-  const long t0 = (long)blockIdx.y * 64;
-  const int c0 = blockIdx.x * 64;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int idx = threadIdx.x + 256 * i, r = idx >> 3, ch = idx & 7;
-    const long t = t0 + r;
-    const int col = c0 + ch * 8;
-    float gv[8], uv[8], o[8];
-    load8<T>(gu + t * ldgu + col, gv);
-    load8<T>(gu + t * ldgu + F + col, uv);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = rnd<T>(silu_f(gv[j])) * uv[j];  // identical to swiglu_fwd_kernel
-    store8<T>(a + t * lda + col, o);
-    put8<T>(&ta[r][swz(r, ch) * 8], o);
-  }
-  __syncthreads();
-  store_tile_t(ta, reinterpret_cast<uint16_t*>(aT), ntok, c0, t0);
-}
-
-template <typename T>
-__global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(const T* __restrict__ dy, T* gu, T* __restrict__ guT,
-                                                           int F, int ldgu, int lddy, long ntok) {
-  __shared__ __attribute__((aligned(16))) uint16_t tg[64][72], tu[64][72];
-  const long t0 = (long)blockIdx.y * 64;
-  const int c0 = blockIdx.x * 64;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int idx = threadIdx.x + 256 * i, r = idx >> 3, ch = idx & 7;
-    const long t = t0 + r;
-    const int col = c0 + ch * 8;
-    float gv[8], uv[8], dv[8], og[8], ou[8];
-    load8<T>(gu + t * ldgu + col, gv);
-    load8<T>(gu + t * ldgu + F + col, uv);
-    load8<T>(dy + t * lddy + col, dv);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {  // identical math / rounding to swiglu_bwd_kernel
-      const float sg = 1.f / (1.f + __expf(-gv[j]));
-      const float a = rnd<T>(gv[j] * sg);
-      const float da = rnd<T>(dv[j] * uv[j]);
-      ou[j] = dv[j] * a;
-      og[j] = da * sg * (1.f + gv[j] * (1.f - sg));
-    }
-    store8<T>(gu + t * ldgu + col, og);
-    store8<T>(gu + t * ldgu + F + col, ou);
-    put8<T>(&tg[r][swz(r, ch) * 8], og);
-    put8<T>(&tu[r][swz(r, ch) * 8], ou);
-  }
-  __syncthreads();
-  store_tile_t(tg, reinterpret_cast<uint16_t*>(guT), ntok, c0, t0);
-  store_tile_t(tu, reinterpret_cast<uint16_t*>(guT), ntok, F + c0, t0);
-}
-
-// Same op, loads hoisted: gu is updated in place, so it cannot be __restrict__, and in the kernel
-// above the compiler may not move iteration 1's loads of gu above iteration 0's stores to it -- each
-// lane has only one row's three 16-B loads in flight at a time. Here every load of the block's
-// NT 64x64 tiles is issued before the first store (NT = 2: 6 x 16 B x 2 in flight per lane, each
-// row 256 contiguous bytes per operand).
+// swiglu_bwd_t: dgu = [dg | du] in place over gu and dguT = dgu^T, same math and rounding as
+// swiglu_bwd_kernel. gu is updated in place, so it cannot be __restrict__ and the compiler may not
+// move a later row's loads of gu above an earlier row's stores: every load of the block's NT 64x64
+// tiles is issued before the first store (NT = 2: 6 x 16 B x 2 in flight per lane, each row 256
+// contiguous bytes per operand; ~10% faster than the register-tile form, which loses occupancy).
 template <typename T, int NT>
 __global__ __launch_bounds__(256) void swiglu_bwd_t_hoist_kernel(const T* __restrict__ dy, T* gu,
                                                                  T* __restrict__ guT, int F, int ldgu, int lddy,
@@ -380,45 +339,8 @@ __global__ __launch_bounds__(256) void swiglu_bwd_t_hoist_kernel(const T* __rest
   }
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void rope_t_kernel(T* x, T* __restrict__ xT, const float2* __restrict__ tab,
-                                                     int ld, int nrot, int D, int S, float sign, long ntok) {
-  __shared__ __attribute__((aligned(16))) uint16_t tile[64][72];
-  const long t0 = (long)blockIdx.y * 64;
-  const int c0 = blockIdx.x * 64;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int idx = threadIdx.x + 256 * i, r = idx >> 3, ch = idx & 7;
-    const long t = t0 + r;
-    const int col = c0 + ch * 8;
-    T* p = x + t * ld + col;
-    float v[8];
-    load8<T>(p, v);
-    if (col < nrot) {  // same math as rope_kernel
-      const int pos = (int)(t % S);
-      const int pi = (col % D) / 2;
-      const float4* tp = reinterpret_cast<const float4*>(tab + (size_t)pos * (D / 2) + pi);
-      const float4 cs01 = tp[0], cs23 = tp[1];
-      const float c[4] = {cs01.x, cs01.z, cs23.x, cs23.z};
-      const float sn[4] = {cs01.y * sign, cs01.w * sign, cs23.y * sign, cs23.w * sign};
-      float o[8];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        rot_pair(v[2 * k], v[2 * k + 1], c[k], sn[k], o[2 * k], o[2 * k + 1]);
-      }
-      store8<T>(p, o);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = o[j];
-    }
-    put8<T>(&tile[r][swz(r, ch) * 8], v);
-  }
-  __syncthreads();
-  store_tile_t(tile, reinterpret_cast<uint16_t*>(xT), ntok, c0, t0);
-}
-
 // ---------------------------------------------------------------------------------------
-// Register-tile versions of the three transposing epilogues (default): one wave per 64-token x
-// 64-column tile, lane (g, ch) owns tokens 8g..8g+7 x columns 8ch..8ch+7, so its eight row
+// Register-tile transposing epilogues (swiglu_fwd_t, rope_t): one wave per 64-token x 64-column tile, lane (g, ch) owns tokens 8g..8g+7 x columns 8ch..8ch+7, so its eight row
 // vectors are the 8x8 block the transposed store needs (transpose8x8_b16). No LDS, no barrier,
 // every operand's eight row loads issued before any math. Same math and rounding as above.
 // tile of this wave (tiles_c column tiles per 64-token row of tiles); false past the end
@@ -470,45 +392,6 @@ __global__ __launch_bounds__(256) void swiglu_fwd_t_reg_kernel(const T* __restri
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void swiglu_bwd_t_reg_kernel(const T* __restrict__ dy, T* gu, T* __restrict__ guT,
-                                                               int F, int ldgu, int lddy, long ntok, long n_tiles) {
-  long t0;
-  int c0, g, ch;
-  if (!wave_tile(F / 64, n_tiles, t0, c0, g, ch)) return;
-  const int col = c0 + 8 * ch;
-  uint4 G[8], U[8], DY[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const long t = t0 + 8 * g + k;
-    G[k] = *reinterpret_cast<const uint4*>(gu + t * ldgu + col);
-    U[k] = *reinterpret_cast<const uint4*>(gu + t * ldgu + F + col);
-    DY[k] = *reinterpret_cast<const uint4*>(dy + t * lddy + col);
-  }
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    float gv[8], uv[8], dv[8], og[8], ou[8];
-    unpack8<T>(G[k], gv);
-    unpack8<T>(U[k], uv);
-    unpack8<T>(DY[k], dv);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float sg = 1.f / (1.f + __expf(-gv[j]));
-      const float av = rnd<T>(gv[j] * sg);
-      const float da = rnd<T>(dv[j] * uv[j]);
-      ou[j] = dv[j] * av;
-      og[j] = da * sg * (1.f + gv[j] * (1.f - sg));
-    }
-    G[k] = pack8<T>(og);  // G/U now hold dg/du
-    U[k] = pack8<T>(ou);
-    const long t = t0 + 8 * g + k;
-    *reinterpret_cast<uint4*>(gu + t * ldgu + col) = G[k];
-    *reinterpret_cast<uint4*>(gu + t * ldgu + F + col) = U[k];
-  }
-  store_t_reg(G, reinterpret_cast<uint16_t*>(guT), ntok, c0, t0, g, ch);
-  store_t_reg(U, reinterpret_cast<uint16_t*>(guT), ntok, F + c0, t0, g, ch);
-}
-
-template <typename T>
 __global__ __launch_bounds__(256) void rope_t_reg_kernel(T* x, T* __restrict__ xT, const float2* __restrict__ tab,
                                                          int ld, int ncols, int nrot, int D, int S, float sign,
                                                          long ntok, long n_tiles) {
@@ -543,28 +426,6 @@ __global__ __launch_bounds__(256) void rope_t_reg_kernel(T* x, T* __restrict__ x
 
 }  // namespace pra
 
-// Which transpose / transposing-epilogue kernels run: by default the register-tile kernels, except
-// swiglu_bwd_t, whose register version (3 operands x 8 rows in flight) loses occupancy and
-// measured ~10% slower than the LDS one (tools/transpose_bench.py, profiles/transpose_ab_s2.log).
-// PYRECOVER_TRANSPOSE=lds / =reg forces one family everywhere (A/B).
-static int pra_transpose_mode() {  // 0 default, 1 lds, 2 reg
-  static const int v = [] {
-    const char* e = getenv("PYRECOVER_TRANSPOSE");
-    if (e && strcmp(e, "lds") == 0) return 1;
-    if (e && strcmp(e, "reg") == 0) return 2;
-    return 0;
-  }();
-  return v;
-}
-static bool pra_use_lds_transpose() { return pra_transpose_mode() == 1; }
-static bool pra_use_lds_swiglu_bwd_t() { return pra_transpose_mode() != 2; }
-// LDS swiglu_bwd_t generation: 0 = one row in flight per lane, 1 = hoisted loads (64x64 tile),
-// 2 = hoisted loads over two 64x64 tiles (default). Read per call (A/B in one process).
-static int pra_swiglu_bwd_hoist() {
-  const char* e = getenv("PRA_SWIGLU_BWD");
-  return e ? atoi(e) : 2;
-}
-
 extern "C" {
 
 hipError_t pra_rope(int dtype, void* x, const void* tab, long ntok, int ld, int ncols, int D, int S,
@@ -588,13 +449,26 @@ hipError_t pra_swiglu_fwd(int dtype, const void* g, const void* u, void* y, long
   return hipGetLastError();
 }
 
+// variant (A/B): 0 = grid-stride kernel, 1 / -1 = hoisted tile kernel, 4 tokens per lane, 2 = 8 per lane
 hipError_t pra_swiglu_bwd(int dtype, const void* dy, const void* g, const void* u, void* dg, void* du,
-                          long ntok, int F, int ldg, int ldu, int lddy, hipStream_t s) {
+                          long ntok, int F, int ldg, int ldu, int lddy, int variant, hipStream_t s) {
   if (F % 8 || ldg % 8 || ldu % 8 || lddy % 8) return hipErrorInvalidValue;
-  const int grid = pra::grid_for((size_t)ntok * (F / 8));
-  PRA_DISPATCH_FLOAT(dtype, T,
-                     hipLaunchKernelGGL((pra::swiglu_bwd_kernel<T>), dim3(grid), dim3(256), 0, s, (const T*)dy,
-                                        (const T*)g, (const T*)u, (T*)dg, (T*)du, ntok, F, ldg, ldu, lddy));
+  if (variant == 0) {
+    const int grid = pra::grid_for((size_t)ntok * (F / 8));
+    PRA_DISPATCH_FLOAT(dtype, T,
+                       hipLaunchKernelGGL((pra::swiglu_bwd_kernel<T>), dim3(grid), dim3(256), 0, s, (const T*)dy,
+                                          (const T*)g, (const T*)u, (T*)dg, (T*)du, ntok, F, ldg, ldu, lddy));
+  } else if (variant == 2) {
+    const dim3 grid((unsigned)((F + 127) / 128), (unsigned)((ntok + 127) / 128));
+    PRA_DISPATCH_FLOAT(dtype, T,
+                       hipLaunchKernelGGL((pra::swiglu_bwd_tile_kernel<T, 8>), grid, dim3(256), 0, s, (const T*)dy,
+                                          (const T*)g, (const T*)u, (T*)dg, (T*)du, ntok, F, ldg, ldu, lddy));
+  } else {
+    const dim3 grid((unsigned)((F + 127) / 128), (unsigned)((ntok + 63) / 64));
+    PRA_DISPATCH_FLOAT(dtype, T,
+                       hipLaunchKernelGGL((pra::swiglu_bwd_tile_kernel<T, 4>), grid, dim3(256), 0, s, (const T*)dy,
+                                          (const T*)g, (const T*)u, (T*)dg, (T*)du, ntok, F, ldg, ldu, lddy));
+  }
   return hipGetLastError();
 }
 
@@ -620,15 +494,9 @@ hipError_t pra_embedding_bwd(int dtype, const int64_t* sorted_ids, const int64_t
 
 hipError_t pra_transpose16(const void* src, void* dst, long R, long C, long ld_src, long ld_dst, hipStream_t s) {
   if (R % 64 || C % 64 || ld_src % 8 || ld_dst % 8) return hipErrorInvalidValue;
-  if (pra_use_lds_transpose()) {
-    dim3 grid((unsigned)(C / 64), (unsigned)(R / 64));
-    hipLaunchKernelGGL((pra::transpose_kernel<uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)src,
-                       (uint16_t*)dst, ld_src, ld_dst);
-  } else {
-    const long n_tiles = (R / 64) * (C / 64);
-    hipLaunchKernelGGL(pra::transpose_reg_kernel, dim3((unsigned)((n_tiles + 3) / 4)), dim3(256), 0, s,
-                       (const uint16_t*)src, (uint16_t*)dst, ld_src, ld_dst, (int)(C / 64), n_tiles);
-  }
+  const long n_tiles = (R / 64) * (C / 64);
+  hipLaunchKernelGGL(pra::transpose_reg_kernel, dim3((unsigned)((n_tiles + 3) / 4)), dim3(256), 0, s,
+                     (const uint16_t*)src, (uint16_t*)dst, ld_src, ld_dst, (int)(C / 64), n_tiles);
   return hipGetLastError();
 }
 
@@ -636,18 +504,10 @@ hipError_t pra_transpose16(const void* src, void* dst, long R, long C, long ld_s
 hipError_t pra_swiglu_fwd_t(int dtype, const void* gu, void* a, void* aT, long ntok, int F, int ldgu, int lda,
                             hipStream_t s) {
   if (ntok % 64 || F % 64 || ldgu % 8 || lda % 8) return hipErrorInvalidValue;
-  if (!pra_use_lds_transpose()) {
-    const long n_tiles = (ntok / 64) * (F / 64);
-    PRA_DISPATCH_16BIT(dtype, T,
-                       hipLaunchKernelGGL((pra::swiglu_fwd_t_reg_kernel<T>), dim3((unsigned)((n_tiles + 3) / 4)),
-                                          dim3(256), 0, s, (const T*)gu, (T*)a, (T*)aT, F, ldgu, lda, ntok,
-                                          n_tiles));
-    return hipGetLastError();
-  }
-  dim3 grid((unsigned)(F / 64), (unsigned)(ntok / 64));
+  const long n_tiles = (ntok / 64) * (F / 64);
   PRA_DISPATCH_16BIT(dtype, T,
-                     hipLaunchKernelGGL((pra::swiglu_fwd_t_kernel<T>), grid, dim3(256), 0, s, (const T*)gu, (T*)a,
-                                        (T*)aT, F, ldgu, lda, ntok));
+                     hipLaunchKernelGGL((pra::swiglu_fwd_t_reg_kernel<T>), dim3((unsigned)((n_tiles + 3) / 4)),
+                                        dim3(256), 0, s, (const T*)gu, (T*)a, (T*)aT, F, ldgu, lda, ntok, n_tiles));
   return hipGetLastError();
 }
 
@@ -655,32 +515,17 @@ hipError_t pra_swiglu_fwd_t(int dtype, const void* gu, void* a, void* aT, long n
 hipError_t pra_swiglu_bwd_t(int dtype, const void* dy, void* gu, void* guT, long ntok, int F, int ldgu, int lddy,
                             hipStream_t s) {
   if (ntok % 64 || F % 64 || ldgu % 8 || lddy % 8) return hipErrorInvalidValue;
-  if (!pra_use_lds_swiglu_bwd_t()) {
-    const long n_tiles = (ntok / 64) * (F / 64);
-    PRA_DISPATCH_16BIT(dtype, T,
-                       hipLaunchKernelGGL((pra::swiglu_bwd_t_reg_kernel<T>), dim3((unsigned)((n_tiles + 3) / 4)),
-                                          dim3(256), 0, s, (const T*)dy, (T*)gu, (T*)guT, F, ldgu, lddy, ntok,
-                                          n_tiles));
-    return hipGetLastError();
-  }
-  const int hoist = pra_swiglu_bwd_hoist();
-  if (hoist == 2 && F % 128 == 0) {
+  if (F % 128 == 0) {
     dim3 grid((unsigned)(F / 128), (unsigned)(ntok / 64));
     PRA_DISPATCH_16BIT(dtype, T,
                        hipLaunchKernelGGL((pra::swiglu_bwd_t_hoist_kernel<T, 2>), grid, dim3(256), 0, s, (const T*)dy,
                                           (T*)gu, (T*)guT, F, ldgu, lddy, ntok));
-    return hipGetLastError();
-  }
-  dim3 grid((unsigned)(F / 64), (unsigned)(ntok / 64));
-  if (hoist) {
+  } else {
+    dim3 grid((unsigned)(F / 64), (unsigned)(ntok / 64));
     PRA_DISPATCH_16BIT(dtype, T,
                        hipLaunchKernelGGL((pra::swiglu_bwd_t_hoist_kernel<T, 1>), grid, dim3(256), 0, s, (const T*)dy,
                                           (T*)gu, (T*)guT, F, ldgu, lddy, ntok));
-    return hipGetLastError();
   }
-  PRA_DISPATCH_16BIT(dtype, T,
-                     hipLaunchKernelGGL((pra::swiglu_bwd_t_kernel<T>), grid, dim3(256), 0, s, (const T*)dy, (T*)gu,
-                                        (T*)guT, F, ldgu, lddy, ntok));
   return hipGetLastError();
 }
 
@@ -688,18 +533,11 @@ hipError_t pra_swiglu_bwd_t(int dtype, const void* dy, void* gu, void* guT, long
 hipError_t pra_rope_t(int dtype, void* x, void* xT, const void* tab, long ntok, int ld, int ncols, int nrot, int D,
                       int S, int inverse, hipStream_t s) {
   if (ntok % 64 || ncols % 64 || nrot % 8 || D % 8 || ld % 8) return hipErrorInvalidValue;
-  if (!pra_use_lds_transpose()) {
-    const long n_tiles = (ntok / 64) * (ncols / 64);
-    PRA_DISPATCH_16BIT(dtype, T,
-                       hipLaunchKernelGGL((pra::rope_t_reg_kernel<T>), dim3((unsigned)((n_tiles + 3) / 4)), dim3(256),
-                                          0, s, (T*)x, (T*)xT, (const float2*)tab, ld, ncols, nrot, D, S,
-                                          inverse ? -1.f : 1.f, ntok, n_tiles));
-    return hipGetLastError();
-  }
-  dim3 grid((unsigned)(ncols / 64), (unsigned)(ntok / 64));
+  const long n_tiles = (ntok / 64) * (ncols / 64);
   PRA_DISPATCH_16BIT(dtype, T,
-                     hipLaunchKernelGGL((pra::rope_t_kernel<T>), grid, dim3(256), 0, s, (T*)x, (T*)xT,
-                                        (const float2*)tab, ld, nrot, D, S, inverse ? -1.f : 1.f, ntok));
+                     hipLaunchKernelGGL((pra::rope_t_reg_kernel<T>), dim3((unsigned)((n_tiles + 3) / 4)), dim3(256), 0,
+                                        s, (T*)x, (T*)xT, (const float2*)tab, ld, ncols, nrot, D, S,
+                                        inverse ? -1.f : 1.f, ntok, n_tiles));
   return hipGetLastError();
 }
 

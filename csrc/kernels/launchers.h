@@ -23,7 +23,7 @@ hipError_t pra_rope(int dtype, void* x, const void* tab, long ntok, int ld, int 
 hipError_t pra_swiglu_fwd(int dtype, const void* g, const void* u, void* y, long ntok, int F, int ldg, int ldu,
                           int ldy, hipStream_t s);
 hipError_t pra_swiglu_bwd(int dtype, const void* dy, const void* g, const void* u, void* dg, void* du, long ntok,
-                          int F, int ldg, int ldu, int lddy, hipStream_t s);
+                          int F, int ldg, int ldu, int lddy, int variant, hipStream_t s);
 hipError_t pra_embedding_fwd(int dtype, const int64_t* ids, const void* W, void* out, long ntok, int D, long V,
                              hipStream_t s);
 hipError_t pra_embedding_bwd(int dtype, const int64_t* sorted_ids, const int64_t* perm, const void* dout, void* dW,
@@ -75,6 +75,6 @@ hipError_t pra_attn_fwd(int dtype, const void* q, const void* k, const void* v, 
 hipError_t pra_attn_bwd(int dtype, const void* q, const void* k, const void* v, const void* o, const void* dout,
                         const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int S, int Hq, int Hkv,
                         int D, long ldq, long ldk, long ldv, long ldo, long lddo, long lddq, long lddk, long lddv,
-                        float scale, int causal, int skv, void* ds_ws, size_t ds_bytes, hipStream_t st);
-size_t pra_attn_bwd_ds_bytes(int B, int S, int Hq, int Hkv, int D, int causal);
+                        float scale, int causal, int skv, const float* rope_tab, hipStream_t st);
+void pra_attn_set_options(int fwd_pipe, float fwd_thr, int dkdv_impl, int dq_pipe);
 }

@@ -118,81 +118,6 @@ __global__ __launch_bounds__(256) void adamw_t_kernel(P* __restrict__ p, const P
   }
 }
 
-// Strip variant: one block walks NT consecutive 64 x 64 tiles of a row band, with the global loads
-// of tile j + 1 issued before tile j is computed and stored (they stay in flight across the
-// tile's barrier), and a double-buffered LDS tile -- the one-tile kernel's blocks each run one
-// load -> barrier -> store episode with nothing in flight around it.
-template <typename P, int NT>
-__global__ __launch_bounds__(256) void adamw_t_strip_kernel(P* __restrict__ p, const P* __restrict__ g,
-                                                            P* __restrict__ m, P* __restrict__ v, P* __restrict__ pt,
-                                                            int rows, int cols, float lr, float b1, float b2, float eps,
-                                                            float wd, float bc1, float bc2_sqrt, float gscale,
-                                                            const float* __restrict__ gscale_dev,
-                                                            const float* __restrict__ hyper_dev) {
-  __shared__ uint16_t tile[2][64][72];
-  const float gs = gscale_dev ? gscale * gscale_dev[0] : gscale;
-  if (hyper_dev) {
-    lr = hyper_dev[0];
-    bc1 = hyper_dev[1];
-    bc2_sqrt = hyper_dev[2];
-  }
-  const float decay = 1.f - lr * wd;
-  const float step_size = lr / bc1;
-  const long r0 = (long)blockIdx.y * 64, cb = (long)blockIdx.x * 64 * NT;
-  uint4 cur[2][4], nxt[2][4];  // [k][p g m v] raw 16-B chunks
-  auto load = [&](uint4 (&d)[2][4], long c0) {
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int idx = threadIdx.x + 256 * k, r = idx >> 3, ch = idx & 7;
-      const long o = (r0 + r) * cols + c0 + 8 * ch;
-      d[k][0] = *reinterpret_cast<const uint4*>(p + o);
-      d[k][1] = *reinterpret_cast<const uint4*>(g + o);
-      d[k][2] = *reinterpret_cast<const uint4*>(m + o);
-      d[k][3] = *reinterpret_cast<const uint4*>(v + o);
-    }
-  };
-  load(cur, cb);
-#pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    const long c0 = cb + 64 * j;
-    if (j + 1 < NT) load(nxt, c0 + 64);
-    uint16_t (*tl)[72] = tile[j & 1];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int idx = threadIdx.x + 256 * k, r = idx >> 3, ch = idx & 7;
-      const long o = (r0 + r) * cols + c0 + 8 * ch;
-      float pv[8], gv[8], mv[8], vv[8];
-      load8<P>(reinterpret_cast<const P*>(&cur[k][0]), pv);
-      load8<P>(reinterpret_cast<const P*>(&cur[k][1]), gv);
-      load8<P>(reinterpret_cast<const P*>(&cur[k][2]), mv);
-      load8<P>(reinterpret_cast<const P*>(&cur[k][3]), vv);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) adamw_elem(pv[e], mv[e], vv[e], gv[e], gs, decay, b1, b2, eps, bc2_sqrt, step_size);
-      store8<P>(p + o, pv);
-      store8<P>(m + o, mv);
-      store8<P>(v + o, vv);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) tl[r][8 * ch + e] = __builtin_bit_cast(uint16_t, from_f<P>(pv[e]));
-    }
-    __syncthreads();  // (tile j & 1 was last read two tiles ago, before the previous barrier)
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int idx = threadIdx.x + 256 * k, c = idx >> 3, rg = idx & 7;
-      uint32_t w[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        w[e] = (uint32_t)tl[8 * rg + 2 * e][c] | ((uint32_t)tl[8 * rg + 2 * e + 1][c] << 16);
-      *reinterpret_cast<uint4*>(pt + (c0 + c) * rows + r0 + 8 * rg) = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-    if (j + 1 < NT) {
-#pragma unroll
-      for (int k = 0; k < 2; ++k)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) cur[k][q] = nxt[k][q];
-    }
-  }
-}
-
 // Sum of squares of a flat buffer -> fp32 partials[gridDim.x]; then a 1-block fixed-order
 // finish computes total norm and clip coefficient min(1, max_norm/(norm+1e-6)).
 template <typename T>
@@ -252,30 +177,14 @@ hipError_t pra_adamw_t(int dtype, void* p, const void* g, void* m, void* v, void
                        float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt, float gscale,
                        const float* gscale_dev, const float* hyper_dev, hipStream_t s) {
   if (rows % 64 || cols % 64 || rows <= 0 || cols <= 0) return hipErrorInvalidValue;
-  // PRA_ADAMW_T_STRIP (read per call): tiles per block of the strip kernel (1 = one-tile kernel,
-  // the default). In isolation 4 tiles per block is faster (7B optimizer step 22.7 -> 21.3 ms,
-  // bit-identical), but overlapped with the backward GEMMs on the side stream its long-lived blocks
-  // cost the step more (1069.6 vs 1074.5 ms, same box; profiles/adamw_t_strip_ab_r2.log).
-  const char* e = getenv("PRA_ADAMW_T_STRIP");
-  int nt = e ? atoi(e) : 1;
-  while (nt > 1 && (cols / 64) % nt) nt /= 2;
-#define PRA_ADAMW_T_LAUNCH(NT)                                                                                  \
-  PRA_DISPATCH_16BIT(dtype, T,                                                                                  \
-                     hipLaunchKernelGGL((pra::adamw_t_strip_kernel<T, NT>), dim3(cols / 64 / NT, rows / 64),   \
-                                        dim3(256), 0, s, (T*)p, (const T*)g, (T*)m, (T*)v, (T*)pt, rows, cols, lr, \
-                                        b1, b2, eps, wd, bc1, bc2_sqrt, gscale, gscale_dev, hyper_dev))
-  if (nt >= 4) {
-    PRA_ADAMW_T_LAUNCH(4);
-  } else if (nt >= 2) {
-    PRA_ADAMW_T_LAUNCH(2);
-  } else {
-    const dim3 grid(cols / 64, rows / 64);
-    PRA_DISPATCH_16BIT(dtype, T,
-                       hipLaunchKernelGGL((pra::adamw_t_kernel<T>), grid, dim3(256), 0, s, (T*)p, (const T*)g, (T*)m,
-                                          (T*)v, (T*)pt, rows, cols, lr, b1, b2, eps, wd, bc1, bc2_sqrt, gscale,
-                                          gscale_dev, hyper_dev));
-  }
-#undef PRA_ADAMW_T_LAUNCH
+  // (A strip kernel walking 4 tiles per block was faster in isolation, 22.7 -> 21.3 ms per 7B step,
+  // but slower overlapped with the backward GEMMs on the side stream: 1074.5 vs 1069.6 ms/step,
+  // profiles/adamw_t_strip_ab_r2.log. Removed.)
+  const dim3 grid(cols / 64, rows / 64);
+  PRA_DISPATCH_16BIT(dtype, T,
+                     hipLaunchKernelGGL((pra::adamw_t_kernel<T>), grid, dim3(256), 0, s, (T*)p, (const T*)g, (T*)m,
+                                        (T*)v, (T*)pt, rows, cols, lr, b1, b2, eps, wd, bc1, bc2_sqrt, gscale,
+                                        gscale_dev, hyper_dev));
   return hipGetLastError();
 }
 

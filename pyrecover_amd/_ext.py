@@ -21,6 +21,7 @@ def native():
         import torch  # noqa: F401  (loads torch's HIP runtime first; our .so binds to it)
         from pyrecover_amd import _C as mod
         _C = mod
+        _apply_attn_env()
         return _C
     except BaseException as e:  # pragma: no cover - exercised only when the build is missing
         _err = e
@@ -60,3 +61,32 @@ def hip16(t) -> bool:
     import torch
 
     return t.is_cuda and t.dtype in (torch.bfloat16, torch.float16)
+
+
+# Attention kernel selection (csrc/kernels/attention.hip AttnOptions): -1 = by shape. The launchers
+# read no environment; PYRECOVER_ATTN_{FWD_PIPE,FWD_THR,DKDV_IMPL,DQ_PIPE} are read once here, when
+# the extension loads, and set_attn_options() changes them between launches (tests, A/B tools).
+_ATTN_DEFAULTS = {"fwd_pipe": -1, "fwd_thr": 8.0, "dkdv_impl": -1, "dq_pipe": -1}
+_attn_opts = dict(_ATTN_DEFAULTS)
+
+
+def _apply_attn_env():
+    env = {}
+    for key, conv in (("fwd_pipe", int), ("fwd_thr", float), ("dkdv_impl", int), ("dq_pipe", int)):
+        v = os.environ.get("PYRECOVER_ATTN_" + key.upper())
+        if v is not None and v != "":
+            env[key] = conv(v)
+    set_attn_options(**env)
+
+
+def set_attn_options(**kw) -> dict:
+    """Set attention kernel selection knobs (fwd_pipe, fwd_thr, dkdv_impl, dq_pipe); keys left out
+    keep their value, ``None`` restores the default. Returns the previous settings."""
+    prev = dict(_attn_opts)
+    for k, v in kw.items():
+        if k not in _ATTN_DEFAULTS:
+            raise KeyError(f"unknown attention option {k!r}")
+        _attn_opts[k] = _ATTN_DEFAULTS[k] if v is None else type(_ATTN_DEFAULTS[k])(v)
+    _C.attn_set_options(_attn_opts["fwd_pipe"], _attn_opts["fwd_thr"], _attn_opts["dkdv_impl"],
+                        _attn_opts["dq_pipe"])
+    return prev

@@ -397,10 +397,13 @@ def _attn_fwd(q, k, v, scale, causal):
     return o.to(q.dtype).contiguous(), None
 
 
-def _attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, causal):
+def _attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, causal, rope_tab=None) -> bool:
+    """Attention backward into dq/dk/dv. With ``rope_tab`` (the forward's RoPE table) the HIP kernels
+    store dq and dk with the inverse rotation already applied; returns whether that happened (the
+    torch path leaves it to the caller)."""
     if lse is not None and _attn_hip(q, k):
-        _ext.require_for(q).attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, causal)
-        return
+        _ext.require_for(q).attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, causal, rope_tab)
+        return rope_tab is not None
     ct = torch.promote_types(q.dtype, torch.float32)
     with torch.enable_grad():
         qq, kk, vv = (t.detach().to(ct).requires_grad_() for t in (q, k, v))
@@ -409,6 +412,7 @@ def _attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, causal):
     dq.copy_(gq)
     dk.copy_(gk)
     dv.copy_(gv)
+    return False
 
 
 class _AttentionBlock(torch.autograd.Function):
@@ -469,16 +473,20 @@ class _AttentionBlock(torch.autograd.Function):
         dq = dqkv[:, :nq].view(B, S, Hq, D)
         dk = dqkv[:, nq:nq + nk].view(B, S, Hkv, D)
         dv = dqkv[:, nq + nk:].view(B, S, Hkv, D)
-        _attn_bwd(q, k, v, o, do, lse, dq, dk, dv, ctx.scale, causal)
+        # the HIP backward applies the inverse RoPE to dq / dk in its epilogue (table rows = positions)
+        use_tab = tab.is_contiguous() and tab.dtype == torch.float32 and tab.shape[0] >= S
+        fused_rope = _attn_bwd(q, k, v, o, do, lse, dq, dk, dv, ctx.scale, causal, tab if use_tab else None)
         if (not _hip_wgrad_ok(dqkv, x2, "qkv") and TN_WGRAD and _tn_ok(dqkv) and _tn_ok(x2) and T % S == 0
                 and D % 8 == 0):
-            # inverse RoPE in place + dqkv^T in one pass, for the K-contiguous weight-grad GEMM
+            # (inverse RoPE in place +) dqkv^T in one pass, for the K-contiguous weight-grad GEMM
             C = _ext.require_for(dqkv)
-            dqkvT = C.rope_t_(dqkv, nq + nk, tab, D, S, True)
+            dqkvT = C.transpose2d(dqkv) if fused_rope else C.rope_t_(dqkv, nq + nk, tab, D, S, True)
             dx = _mm_dgrad(dqkv, w_qkv, w_qkv_t, "qkv_d")
             slot_qkv.mm_(dqkvT, C.transpose2d(x2).t(), tuple(w_qkv.shape))
         else:
-            if _ext.hip(dqkv) and D % 8 == 0:
+            if fused_rope:
+                pass  # dq / dk already un-rotated by the attention backward
+            elif _ext.hip(dqkv) and D % 8 == 0:
                 _ext.require_for(dqkv).rope_(dqkv, nq + nk, tab, D, S, 0, True)
             else:
                 ref.rope_inplace_2d(dqkv, nq + nk, tab, D, S, inverse=True)

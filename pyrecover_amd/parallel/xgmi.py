@@ -40,6 +40,23 @@ import torch.distributed as dist
 from .. import _ext
 
 
+
+def _device_identity(i: int) -> str:
+    """Stable identity of visible device i across processes (UUID, else PCI address)."""
+    p = torch.cuda.get_device_properties(i)
+    u = getattr(p, "uuid", None)
+    if u is not None and str(u).strip("0-") != "":
+        return str(u)
+    pci = tuple(getattr(p, a, None) for a in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+    if any(x is not None for x in pci):
+        return "pci:%s:%s:%s" % pci
+    return f"{p.name}#{i}"
+
+
+def _hidden_ranks(vis) -> List[int]:
+    """Ranks whose GPU some rank cannot see; vis[r] = (rank r's device identity, identities rank r sees)."""
+    return sorted({r for r, (own, _) in enumerate(vis) for _, seen in vis if own not in seen})
+
 class _Work:
     __slots__ = ("owner", "b", "ready")
 
@@ -129,17 +146,22 @@ class XgmiAllReduce:
         # 1) CPU barriers for the comm thread (its own gloo group, used by nothing else)
         self.hgroup = dist.new_group(backend="gloo")
         # 2) every peer GPU must be visible to map its buffer: under SLURM per-task isolation
-        # (--gpus-per-task=1 / --gpu-bind) each rank sees one device and peer IPC cannot work.
+        # (--gpus-per-task=1 / --gpu-bind) each rank sees only its own device and peer IPC cannot
+        # work. Devices are compared by identity (UUID / PCI address), not by index, so ranks that
+        # share one GPU (one-GPU rehearsals) pass and isolated ranks that all see "device 0" do not.
         # Decided collectively, so every rank raises instead of one rank hanging the others.
         n_vis = torch.cuda.device_count()
+        mine = (_device_identity(di), [_device_identity(i) for i in range(n_vis)])
         vis: List = [None] * W
-        dist.all_gather_object(vis, n_vis, group=self.hgroup)
-        if min(vis) < W:
+        dist.all_gather_object(vis, mine, group=self.hgroup)
+        hidden = _hidden_ranks(vis)
+        if hidden:
             raise RuntimeError(
-                f"xgmi all-reduce needs all {W} node GPUs visible to every rank (visible per rank: {vis}); "
-                "per-task GPU isolation (srun --gpus-per-task=1 / --gpu-bind, or per-rank "
-                "ROCR_VISIBLE_DEVICES) hides the peers. Use the default RCCL all-reduce "
-                "(--allreduce rccl) or launch with every GPU visible.")
+                f"xgmi all-reduce needs every rank's GPU visible to every rank (GPUs of ranks {hidden} are "
+                f"hidden from some peers; visible per rank: {[len(s) for _, s in vis]}); per-task GPU "
+                "isolation (srun --gpus-per-task=1 / --gpu-bind, or per-rank ROCR_VISIBLE_DEVICES) hides "
+                "the peers. Use the default RCCL all-reduce (--allreduce rccl) or launch with every GPU "
+                "visible.")
         # 3) exportable gradient buffer
         buf = self.C.ipc_empty(flat.grad.numel(), self.dtype, di)
         buf.copy_(flat.grad)

@@ -23,3 +23,13 @@ def cuda():
 
     _ext.native()  # GPU tests must exercise the HIP path: fail loudly if it is missing
     return torch.device("cuda", 0)
+
+
+@pytest.fixture
+def attn_opts(cuda):
+    """Setter for the attention kernel selection (pyrecover_amd._ext.set_attn_options); every
+    option is restored to its default after the test."""
+    from pyrecover_amd import _ext
+
+    yield _ext.set_attn_options
+    _ext.set_attn_options(fwd_pipe=None, fwd_thr=None, dkdv_impl=None, dq_pipe=None)

@@ -274,3 +274,14 @@ def test_checkpoint_restores_each_ranks_own_rng(tmp_path, fmt):
         ck = torch.load(tmp_path / "ckpt_1.pt", weights_only=False)
         assert {"epoch", "step", "model", "optimizer"} <= set(ck)
         assert len(ck["pyrecover_state"]["rng_per_rank"]) == 2
+
+
+def test_xgmi_visibility_check_compares_device_identity():
+    """Per-task isolation (each rank sees only its own GPU as index 0) is refused; ranks sharing one
+    GPU (one-GPU rehearsal) and a node with every GPU visible pass."""
+    from pyrecover_amd.parallel.xgmi import _hidden_ranks
+
+    assert _hidden_ranks([("A", ["A"]), ("B", ["B"])]) == [0, 1]
+    assert _hidden_ranks([("A", ["A"]), ("A", ["A"])]) == []
+    assert _hidden_ranks([("A", ["A", "B"]), ("B", ["A", "B"])]) == []
+    assert _hidden_ranks([("A", ["A", "B"]), ("B", ["B"])]) == [0]

@@ -188,11 +188,10 @@ def _qkv(cuda, B, S, Hq, Hkv, D, seed=0, scale=1.0):
 @pytest.mark.parametrize("B,S,Hq,Hkv,D", [(1, 256, 4, 4, 128), (2, 512, 8, 2, 128), (1, 384, 4, 1, 64),
                                           (1, 128, 2, 2, 64), (1, 192, 4, 2, 128)])
 @pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("pipe", ["0", "1", "bal"])
-def test_attention_fwd(cuda, monkeypatch, pipe, B, S, Hq, Hkv, D, causal):
-    """Every forward kernel (PRA_FWD_PIPE: fwd_kernel / cross-tile pipelined fwd_p_kernel, and the
-    pipelined kernel with its exponentials split between its phases, PRA_FWD_BAL)."""
-    _fwd_variant(monkeypatch, pipe)
+@pytest.mark.parametrize("pipe", [0, 1])
+def test_attention_fwd(cuda, attn_opts, pipe, B, S, Hq, Hkv, D, causal):
+    """Both forward kernels (fwd_pipe: fwd_kernel / cross-tile pipelined fwd_p_kernel)."""
+    attn_opts(fwd_pipe=pipe)
     C = _ext.native()
     _, q, k, v = _qkv(cuda, B, S, Hq, Hkv, D)
     scale = 1 / math.sqrt(D)
@@ -202,18 +201,12 @@ def test_attention_fwd(cuda, monkeypatch, pipe, B, S, Hq, Hkv, D, causal):
     assert (lse - lse_ref).abs().max().item() < 1e-3
 
 
-def _fwd_variant(monkeypatch, pipe):
-    monkeypatch.setenv("PRA_FWD_PIPE", "1" if pipe == "bal" else pipe)
-    monkeypatch.setenv("PRA_FWD_BAL", "1" if pipe == "bal" else "0")
-
-
-@pytest.mark.parametrize("pipe", ["0", "1", "bal"])
-@pytest.mark.parametrize("thr", ["0", "8"])
-def test_attention_fwd_rescale_spike(cuda, monkeypatch, pipe, thr):
+@pytest.mark.parametrize("pipe", [0, 1])
+@pytest.mark.parametrize("thr", [0.0, 8.0])
+def test_attention_fwd_rescale_spike(cuda, attn_opts, pipe, thr):
     """Forces the online-softmax running max to jump at a late key tile (rule 26), with the exact
-    rescale (PRA_FWD_THR=0) and the default deferred threshold."""
-    _fwd_variant(monkeypatch, pipe)
-    monkeypatch.setenv("PRA_FWD_THR", thr)
+    rescale (fwd_thr=0) and the default deferred threshold."""
+    attn_opts(fwd_pipe=pipe, fwd_thr=thr)
     C = _ext.native()
     B, S, H, D = 1, 512, 2, 128
     _, q, k, v = _qkv(cuda, B, S, H, H, D, seed=3)
@@ -254,15 +247,14 @@ def test_attention_bwd(cuda, B, S, Hq, Hkv, D, causal):
     assert torch.equal(dqkv, dqkv2)
 
 
-@pytest.mark.parametrize("impl", ["0", "1"])
+@pytest.mark.parametrize("impl", [0, 1])
 @pytest.mark.parametrize("B,S,Hq,Hkv,D,causal", [(1, 1024, 4, 1, 128, True), (2, 512, 4, 2, 128, False),
                                                  (1, 640, 2, 2, 64, True)])
-def test_attention_bwd_dkdv_kernels(cuda, monkeypatch, impl, B, S, Hq, Hkv, D, causal):
+def test_attention_bwd_dkdv_kernels(cuda, attn_opts, impl, B, S, Hq, Hkv, D, causal):
     """Both backward kernel generations -- dK/dV two-wave vs one-wave-per-SIMD pipelined
-    (PRA_DKDV_IMPL), dQ plain vs region-pipelined (PRA_DQ_PIPE) -- against the fp32 oracle, with
+    (dkdv_impl), dQ plain vs region-pipelined (dq_pipe) -- against the fp32 oracle, with
     multi-step loops, GQA and the causal diagonal."""
-    monkeypatch.setenv("PRA_DKDV_IMPL", impl)
-    monkeypatch.setenv("PRA_DQ_PIPE", impl)
+    attn_opts(dkdv_impl=impl, dq_pipe=impl)
     C = _ext.native()
     _, q, k, v = _qkv(cuda, B, S, Hq, Hkv, D, seed=5)
     scale = 1 / math.sqrt(D)
@@ -280,32 +272,56 @@ def test_attention_bwd_dkdv_kernels(cuda, monkeypatch, impl, B, S, Hq, Hkv, D, c
     assert torch.equal(dq, dq2) and torch.equal(dk, dk2) and torch.equal(dv, dv2)
 
 
-@pytest.mark.parametrize("B,S,Hq,Hkv", [(1, 1024, 4, 1), (2, 512, 4, 4), (1, 2048, 2, 2)])
-def test_attention_bwd_materialized_ds(cuda, monkeypatch, B, S, Hq, Hkv):
-    """dS-materializing backward (PRA_ATTN_DS=1: dK/dV also writes dS, dQ is one GEMM over it) vs
-    the fp32 oracle; dK/dV bit-identical to the default path, dQ deterministic."""
-    monkeypatch.setenv("PRA_DKDV_IMPL", "0")
-    monkeypatch.setenv("PRA_ATTN_DELTA_PRE", "1")  # same delta = rowsum(dO*O) kernel as the dS path
+@pytest.mark.parametrize("impl", [0, 1])
+@pytest.mark.parametrize("B,S,Hq,Hkv,D,causal", [(2, 512, 8, 2, 128, True), (1, 384, 4, 1, 64, True),
+                                                 (1, 256, 4, 4, 128, False), (1, 1000, 4, 2, 128, True)])
+def test_attention_bwd_fused_inverse_rope(cuda, attn_opts, impl, B, S, Hq, Hkv, D, causal):
+    """attn_bwd(..., rope_tab): dq / dk leave the kernels with the inverse RoPE applied (fp32, rounded
+    once) -- against the fp32 oracle of the unfused op (backward + inverse rotation), for both dK/dV
+    kernels, GQA, D = 64 and a padded (untiled) sequence; dv is bitwise the unfused one."""
+    from pyrecover_amd.ops.reference import precompute_freqs_cis, rope_table
+
+    attn_opts(dkdv_impl=impl, dq_pipe=impl)
     C = _ext.native()
-    _, q, k, v = _qkv(cuda, B, S, Hq, Hkv, 128, seed=11)
-    scale = 1 / math.sqrt(128)
-    o, lse = C.attn_fwd(q, k, v, scale, True)
-    do = torch.randn(B, S, Hq, 128, device=cuda).bfloat16()
-    outs = {}
-    for ds in ("0", "1", "1"):
-        monkeypatch.setenv("PRA_ATTN_DS", ds)
-        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
-        C.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, True)
-        if ds in outs:
-            assert all(torch.equal(a, b) for a, b in zip(outs[ds], (dq, dk, dv)))  # deterministic
-        outs[ds] = (dq, dk, dv)
+    _, q, k, v = _qkv(cuda, B, S, Hq, Hkv, D, seed=9)
+    scale = 1 / math.sqrt(D)
+    tab = rope_table(precompute_freqs_cis(D, S + 64, 10000.0)).to(cuda)  # longer table: rows = positions
+    o, lse = C.attn_fwd(q, k, v, scale, causal)
+    do = torch.randn(B, S, Hq, D, device=cuda).bfloat16()
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    C.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, causal, tab)
+    dq0, dk0, dv0 = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    C.attn_bwd(q, k, v, o, do, lse, dq0, dk0, dv0, scale, causal)
+    assert torch.equal(dv, dv0)
     qf, kf, vf = (t.float().requires_grad_() for t in (q, k, v))
-    of, _ = R.attention_lse_ref(qf, kf, vf, True, scale)
+    of, _ = R.attention_lse_ref(qf, kf, vf, causal, scale)
     of.backward(do.float())
-    for got, want in zip(outs["1"], (qf.grad, kf.grad, vf.grad)):
-        assert _rel(got, want) < 3e-2, (_rel(got, want))
-    assert torch.equal(outs["1"][1], outs["0"][1]) and torch.equal(outs["1"][2], outs["0"][2])
-    assert _rel(outs["1"][0], outs["0"][0].float()) < 1e-2
+    for got, g32, H in ((dq, qf.grad, Hq), (dk, kf.grad, Hkv)):
+        want = g32.reshape(B * S, H * D).clone()
+        R.rope_inplace_2d(want, H * D, tab, D, S, inverse=True)
+        assert _rel(got, want.view(B, S, H, D)) < 3e-2, _rel(got, want.view(B, S, H, D))
+    # identical to the separate inverse-RoPE pass up to one bf16 rounding of the unrotated values
+    for got, base, H in ((dq, dq0, Hq), (dk, dk0, Hkv)):
+        sep = base.reshape(B * S, H * D).clone()
+        C.rope_(sep, H * D, tab, D, S, 0, True)
+        assert _rel(got, sep.view(B, S, H, D).float()) < 1e-2
+
+
+@pytest.mark.parametrize("T,F,dtype", [(4096, 1024, torch.bfloat16), (1000, 392, torch.bfloat16),
+                                       (512, 256, torch.float16), (256, 136, torch.float32)])
+def test_swiglu_bwd_variants_bitwise(cuda, T, F, dtype):
+    """The hoisted tile kernels (4 and 8 tokens per lane, partial row / column tiles) equal the
+    grid-stride kernel bit for bit, in place over gu and out of place."""
+    C_ = _ext.native()
+    torch.manual_seed(T + F)
+    gu = torch.randn(T, 2 * F, device=cuda).to(dtype)
+    dy = torch.randn(T, F, device=cuda).to(dtype)
+    ref = C_.swiglu_bwd(dy, gu, None, 0)
+    for var in (1, 2, -1):
+        assert torch.equal(C_.swiglu_bwd(dy, gu, None, var), ref)
+        g2 = gu.clone()
+        C_.swiglu_bwd(dy, g2, g2, var)
+        assert torch.equal(g2, ref)
 
 
 def test_single_hip_runtime_loaded(cuda):
@@ -324,13 +340,10 @@ def test_transpose2d_exact(cuda, R, C):
     assert torch.equal(C_.transpose2d(xs), xs.t().contiguous())
 
 
-@pytest.mark.parametrize("gen", ["0", "1", "2"])
 @pytest.mark.parametrize("T,F,dtype", [(256, 192, torch.bfloat16), (64, 192, torch.bfloat16),
                                        (2048, 1024, torch.bfloat16), (128, 256, torch.float16)])
-def test_swiglu_bwd_t_matches_swiglu_bwd_exactly(cuda, T, F, dtype, gen, monkeypatch):
-    # every LDS generation (PRA_SWIGLU_BWD, read per call; F = 192 makes generation 2 fall back to
-    # the one-tile kernel) against the row-major kernel
-    monkeypatch.setenv("PRA_SWIGLU_BWD", gen)
+def test_swiglu_bwd_t_matches_swiglu_bwd_exactly(cuda, T, F, dtype):
+    # two-tile kernel (F % 128 == 0) and its one-tile fallback (F = 192) against the row-major kernel
     C_ = _ext.native()
     gu = torch.randn(T, 2 * F, device=cuda).to(dtype)
     dy = torch.randn(T, F, device=cuda).to(dtype)
@@ -352,8 +365,8 @@ def test_swiglu_fwd_t_matches_swiglu_fwd_exactly(cuda, T, F):
 
 
 def test_attention_bwd_delta_many_heads(cuda):
-    """Backward preprocess (delta = rowsum(dO * O), staged per query block in LDS) with a head count
-    that is not a power of two and D = 64: dq/dk/dv against the fp32 oracle."""
+    """delta = rowsum(dO * O) (computed by the dQ kernel) with a head count that is not a power of
+    two and D = 64: dq/dk/dv against the fp32 oracle."""
     C = _ext.native()
     B, S, Hq, Hkv, D = 1, 128, 12, 12, 64
     q, k, v = (torch.randn(B, S, H, D, device=cuda).bfloat16() for H in (Hq, Hkv, Hkv))
@@ -387,12 +400,9 @@ def test_rope_t_matches_rope_exactly(cuda):
 
 @pytest.mark.parametrize("rows,cols", [(64, 64), (192, 320), (4096, 128), (128, 512)])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("strip", ["1", "4"])
-def test_adamw_t_matches_flat_adamw_plus_transpose(cuda, monkeypatch, strip, rows, cols, dtype):
+def test_adamw_t_matches_flat_adamw_plus_transpose(cuda, rows, cols, dtype):
     """Fused AdamW + transposed-shadow write == flat AdamW followed by transpose2d, bit for bit
-    (incl. device-side grad scale and hyper-parameters), for the one-tile and the strip kernel
-    (PRA_ADAMW_T_STRIP; 4 falls back to 2 / 1 tiles per block when cols/64 is not divisible)."""
-    monkeypatch.setenv("PRA_ADAMW_T_STRIP", strip)
+    (incl. device-side grad scale and hyper-parameters)."""
     C = _ext.native()
     torch.manual_seed(rows + cols)
     p = torch.randn(rows, cols, device=cuda).to(dtype)
