@@ -513,6 +513,19 @@ void wgrad_mm_(const at::Tensor& a, const at::Tensor& b, at::Tensor out, bool ac
         "wgrad_mm");
 }
 
+// timing experiments of the weight-gradient kernel (results are garbage; tools/gemm_exp.py)
+void wgrad_mm_exp_(const at::Tensor& a, const at::Tensor& b, at::Tensor out, int64_t exp) {
+  check_dev(a, "a");
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16,
+              "wgrad_mm_exp: bf16");
+  const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
+  TORCH_CHECK(b.size(0) == K && out.size(0) == M && out.size(1) == N, "wgrad_mm_exp: shapes");
+  const c10::DeviceGuard guard(a.device());
+  check(pra_wgrad_gemm_exp(a.data_ptr(), b.data_ptr(), out.data_ptr(), (int)M, (int)N, (int)K, a.stride(0), b.stride(0),
+                           out.stride(0), (int)exp, stream_of(a)),
+        "wgrad_mm_exp");
+}
+
 // NT GEMM with a fused epilogue (gemm_nt.hip): a [M, K], b [N, K] row-major (K-contiguous).
 //   epi 0: out [M, N] = a b^T
 //   epi 1: SwiGLU forward, b = W1|W3 [2F, K]: out = gu [M, 2F], out2 = a [M, F]
@@ -752,6 +765,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("gscale"), py::arg("gscale_dev") = py::none(), py::arg("hyper_dev") = py::none());
   m.def("grad_norm", &grad_norm);
   m.def("wgrad_mm_", &wgrad_mm_);
+  m.def("wgrad_mm_exp_", &wgrad_mm_exp_);
   m.def("gemm_nt_", &gemm_nt_, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("epi") = 0,
         py::arg("out2") = py::none(), py::arg("tab") = py::none(), py::arg("S") = 0, py::arg("D") = 0,
         py::arg("nrot") = 0);

@@ -61,7 +61,9 @@ __device__ __forceinline__ i16x4 tr4(const T* tile, int byte_off) {
 // ws and takes a ticket; the last arriver of a tile sums the S partials in part order (its own from
 // ws too) -- deterministic, and nothing ever waits on another
 // workgroup.
-template <typename T, bool ACC>
+// EXP (timing experiments only, tools/gemm_exp.py; results are garbage): bit 0 = no main-loop
+// LDS-DMA (prologue stages only), bit 1 = no main-loop fragment reads (stale registers)
+template <typename T, bool ACC, int EXP = 0>
 __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, const T* __restrict__ B,
                                                       T* __restrict__ C, int M, int N, int K, long lda, long ldb,
                                                       long ldc, float* __restrict__ ws, int* __restrict__ tickets,
@@ -153,14 +155,16 @@ __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, c
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[i][j] = mfma16(cb[j], ca[i], acc[i][j]);
-      wait_vm<2 * NI * (NS - 3)>();  // stage kt + 1 landed
+      if constexpr (!(EXP & 1)) wait_vm<2 * NI * (NS - 3)>();  // stage kt + 1 landed
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       const int kd = min(kt + NS - 1, k1 - 1);
 #pragma unroll
       for (int gi = 0; gi < 8; ++gi) {
-        na[gi] = fragA(nta, gi);
-        nb[gi] = fragB(nta + TILE, gi);
+        if constexpr (!(EXP & 2)) {
+          na[gi] = fragA(nta, gi);
+          nb[gi] = fragB(nta + TILE, gi);
+        }
         const int i = 4 + (gi >> 1);
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
@@ -172,7 +176,7 @@ __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, c
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         }
-        dma(sd, kd, gi);
+        if constexpr (!(EXP & 1)) dma(sd, kd, gi);
       }
     };
     // unrolled by lcm(NS, 2) = 10: compile-time ring slot and fragment register set
@@ -335,6 +339,27 @@ hipError_t pra_wgrad_gemm(int dtype, const void* A, const void* B, void* C, int 
     return hipErrorInvalidValue;
   }
 #undef PRA_WG_LAUNCH
+  return hipGetLastError();
+}
+
+// timing experiments (see wgrad16_kernel's EXP): bf16, no accumulate, no split tail. Measured at
+// 32768 x 4096 x 16384: 1.40 PF as is, 1.78 PF without the main-loop LDS-DMA, 1.53 PF without the
+// fragment reads (profiles/r3/gemm_wgrad_exp.log)
+hipError_t pra_wgrad_gemm_exp(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb,
+                              long ldc, int exp, hipStream_t s) {
+  using namespace pra::gm;
+  if (M % BM || N % BN || K % BK || K <= 0 || lda % 8 || ldb % 8 || ldc % 8) return hipErrorInvalidValue;
+  const dim3 grid((M / BM) * (N / BN)), block(NTH);
+#define PRA_WG_EXP(E)                                                                                        \
+  hipLaunchKernelGGL((pra::wg::wgrad16_kernel<__bf16, false, E>), grid, block, 0, s, (const __bf16*)A,         \
+                     (const __bf16*)B, (__bf16*)C, M, N, K, lda, ldb, ldc, nullptr, nullptr, 0, 1)
+  switch (exp) {
+    case 1: PRA_WG_EXP(1); break;
+    case 2: PRA_WG_EXP(2); break;
+    case 3: PRA_WG_EXP(3); break;
+    default: PRA_WG_EXP(0); break;
+  }
+#undef PRA_WG_EXP
   return hipGetLastError();
 }
 

@@ -40,6 +40,8 @@ hipError_t pra_transpose16(const void* src, void* dst, long R, long C, long ld_s
 // M, N multiples of 256, K of 32 (gemm_wgrad.hip)
 hipError_t pra_wgrad_gemm(int dtype, const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb,
                           long ldc, int accumulate, float* ws, int* tickets, int cus, hipStream_t s);
+hipError_t pra_wgrad_gemm_exp(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb,
+                              long ldc, int exp, hipStream_t s);
 long pra_wgrad_ws_floats(int M, int N, int K, int cus);
 int pra_wgrad_ticket_count(int M, int N, int K, int cus);
 // C = A B^T, A [M][K], B [N][K] (both K-contiguous) with a fused epilogue (gemm_nt.hip):

@@ -83,6 +83,11 @@ def _mm_into(slot, a, b, shape):
 # activations, which is worth two bandwidth-bound HIP transposes for the large projections
 # (QKV, output projection, W1|W3, W2, output head; tools/gemm_bench.py --layouts).
 # PYRECOVER_TN_WGRAD=0 disables it.
+# SwiGLU backward kernel (csrc/kernels/elementwise.hip pra_swiglu_bwd): -1 = default (hoisted tile
+# kernel), 0 = grid-stride kernel (A/B: tools/step_ab.py)
+SWIGLU_BWD_VARIANT = int(os.environ.get("PYRECOVER_SWIGLU_BWD", "-1"))
+# inverse RoPE of dq / dk in the attention backward's epilogue (else a separate pass over dq|dk)
+FUSED_ROPE_BWD = os.environ.get("PYRECOVER_FUSED_ROPE_BWD", "1") == "1"
 TN_WGRAD = os.environ.get("PYRECOVER_TN_WGRAD", "1") == "1"
 TN_WGRAD_WO = TN_WGRAD and os.environ.get("PYRECOVER_TN_WGRAD_WO", "1") == "1"
 
@@ -474,7 +479,7 @@ class _AttentionBlock(torch.autograd.Function):
         dk = dqkv[:, nq:nq + nk].view(B, S, Hkv, D)
         dv = dqkv[:, nq + nk:].view(B, S, Hkv, D)
         # the HIP backward applies the inverse RoPE to dq / dk in its epilogue (table rows = positions)
-        use_tab = tab.is_contiguous() and tab.dtype == torch.float32 and tab.shape[0] >= S
+        use_tab = FUSED_ROPE_BWD and tab.is_contiguous() and tab.dtype == torch.float32 and tab.shape[0] >= S
         fused_rope = _attn_bwd(q, k, v, o, do, lse, dq, dk, dv, ctx.scale, causal, tab if use_tab else None)
         if (not _hip_wgrad_ok(dqkv, x2, "qkv") and TN_WGRAD and _tn_ok(dqkv) and _tn_ok(x2) and T % S == 0
                 and D % 8 == 0):
@@ -513,7 +518,7 @@ def _swiglu_fwd(gu):
 
 def _swiglu_bwd_(da, gu):
     if _vec_hip(gu, gu.shape[1] // 2) and gu.shape[1] % 16 == 0:
-        return _ext.require_for(gu).swiglu_bwd(da, gu, gu)
+        return _ext.require_for(gu).swiglu_bwd(da, gu, gu, SWIGLU_BWD_VARIANT)
     F = gu.shape[1] // 2
     dg, du = ref.swiglu_bwd_ref(da, gu[:, :F], gu[:, F:])
     gu[:, :F] = dg
