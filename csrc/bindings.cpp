@@ -766,8 +766,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("grad_norm", &grad_norm);
   m.def("wgrad_mm_", &wgrad_mm_);
   m.def("wgrad_mm_exp_", &wgrad_mm_exp_);
-  m.def("gemm_nt_set_sched", [](int sched) { pra_gemm_nt_set_sched(sched); },
-        "NT GEMM schedule (A/B): 0 = 64-deep chunk ring, 1 = 32-deep ring, balanced schedule");
   m.def("gemm_nt_", &gemm_nt_, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("epi") = 0,
         py::arg("out2") = py::none(), py::arg("tab") = py::none(), py::arg("S") = 0, py::arg("D") = 0,
         py::arg("nrot") = 0);

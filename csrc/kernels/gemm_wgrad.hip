@@ -62,8 +62,7 @@ __device__ __forceinline__ i16x4 tr4(const T* tile, int byte_off) {
 // ws too) -- deterministic, and nothing ever waits on another
 // workgroup.
 // EXP (timing experiments only, tools/gemm_exp.py; results are garbage): bit 0 = no main-loop
-// LDS-DMA (prologue stages only), bit 1 = no main-loop fragment reads (stale registers), bit 2 = the
-// balanced schedule (fragment reads and DMA spread over the whole step, barrier at its start)
+// LDS-DMA (prologue stages only), bit 1 = no main-loop fragment reads (stale registers)
 template <typename T, bool ACC, int EXP = 0>
 __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, const T* __restrict__ B,
                                                       T* __restrict__ C, int M, int N, int K, long lda, long ldb,
@@ -152,38 +151,6 @@ __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, c
     auto step = [&](auto s_c, V8<T> (&ca)[8], V8<T> (&cb)[8], V8<T> (&na)[8], V8<T> (&nb)[8], int kt) {
       constexpr int s = decltype(s_c)::value % NS, sn = (s + 1) % NS, sd = (s + NS - 1) % NS;
       const T* nta = smem + sn * 2 * TILE;
-      if constexpr (EXP & 4) {
-        // balanced: wait + barrier at the step's start (stage kt + 1 published, stage kt - 1's slot
-        // free), then 16 groups of 4 MFMAs, each with one fragment read of stage kt + 1 (order B0..7,
-        // A0..7: the next step's first MFMAs use the oldest) and every other group one DMA
-        if constexpr (!(EXP & 1)) wait_vm<2 * NI * (NS - 3)>();
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        const int kd = min(kt + NS - 1, k1 - 1);
-#pragma unroll
-        for (int g = 0; g < 16; ++g) {
-          if constexpr (!(EXP & 2)) {
-            if (g < 8)
-              nb[g] = fragB(nta + TILE, g);
-            else
-              na[g - 8] = fragA(nta, g - 8);
-          }
-          const int i = g >> 1;
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) {
-            const int j = 4 * (g & 1) + jj;
-            acc[i][j] = mfma16(cb[j], ca[i], acc[i][j]);
-          }
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-          if constexpr (!(EXP & 1))
-            if (g & 1) dma(sd, kd, g >> 1);
-        }
-        return;
-      }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -390,9 +357,6 @@ hipError_t pra_wgrad_gemm_exp(const void* A, const void* B, void* C, int M, int 
     case 1: PRA_WG_EXP(1); break;
     case 2: PRA_WG_EXP(2); break;
     case 3: PRA_WG_EXP(3); break;
-    case 4: PRA_WG_EXP(4); break;
-    case 5: PRA_WG_EXP(5); break;
-    case 6: PRA_WG_EXP(6); break;
     default: PRA_WG_EXP(0); break;
   }
 #undef PRA_WG_EXP

@@ -47,7 +47,6 @@ int pra_wgrad_ticket_count(int M, int N, int K, int cus);
 // C = A B^T, A [M][K], B [N][K] (both K-contiguous) with a fused epilogue (gemm_nt.hip):
 // epi 0 plain, 1 SwiGLU forward (C = gu [M][2F], c2 = a [M][F]), 2 SwiGLU backward in place over
 // gu (C), 3 RoPE on the first nrot columns (tab float2 [S][D/2])
-void pra_gemm_nt_set_sched(int sched);
 hipError_t pra_gemm_nt(int dtype, int epi, const void* A, const void* B, void* C, int M, int N, int K, long lda,
                        long ldb, long ldc, void* c2, long ldc2, int F, const void* tab, int S, int D, int nrot,
                        float* ws, int* tickets, int cus, hipStream_t s);

@@ -37,14 +37,9 @@ def main():
     y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     w = torch.randn(N, K, device=dev, generator=g).bfloat16()
     xa = torch.randn(M, K, device=dev, generator=g).bfloat16()
-
-    def nt(sched):
-        C.gemm_nt_set_sched(sched)
-        C.gemm_nt_(xa, w, y)
-        C.gemm_nt_set_sched(0)
     arms = {"lib_tn": lambda: torch.mm(dyt, xt.t()), "lib_nt": lambda: torch.mm(xa, w.t()),
-            "nt": lambda: nt(0), "nt_bal": lambda: nt(1)}
-    for e in range(7):  # 4..6: the balanced schedule (+ the same removals)
+            "nt": lambda: C.gemm_nt_(xa, w, y)}
+    for e in range(4):
         arms[f"exp{e}"] = (lambda e=e: C.wgrad_mm_exp_(dy, x, y, e))
     t = {k: [] for k in arms}
     for f in arms.values():
