@@ -623,9 +623,9 @@ void check_bshd(const at::Tensor& t, const char* name, int64_t B, int64_t S, int
 }
 
 void check_attn_dtype(const at::Tensor& q) {
-  TORCH_CHECK(q.scalar_type() == at::kBFloat16 || q.scalar_type() == at::kHalf,
-              "attention: the HIP kernels take bf16 or fp16 (got ", q.scalar_type(),
-              "); fp32/fp64 models run the attention in torch (pyrecover_amd.ops.fused)");
+  TORCH_CHECK(q.scalar_type() == at::kBFloat16 || q.scalar_type() == at::kHalf || q.scalar_type() == at::kFloat,
+              "attention: the HIP kernels take bf16, fp16 or fp32 (got ", q.scalar_type(),
+              "); fp64 models run the attention in torch (pyrecover_amd.ops.fused)");
 }
 
 // Sequences that do not tile (S % 64 forward, S % 128 backward) run on zero-padded copies of
@@ -655,7 +655,8 @@ std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const
   TORCH_CHECK(Hq % Hkv == 0, "attention: n_heads must be a multiple of n_kv_heads");
   TORCH_CHECK(S > 0 && (S % 64 == 0 || S <= (int64_t)INT32_MAX - kSeqPad), "attention: bad seq_len");
   const c10::DeviceGuard guard(q.device());
-  if (S % 64) {
+  const int64_t fwd_tile = q.scalar_type() == at::kFloat ? 128 : 64;  // fp32 kernel: 128-query blocks
+  if (S % fwd_tile) {
     const int64_t Sp = round_up(S, kSeqPad);
     at::Tensor qp = pad_seq(q, Sp), kp = pad_seq(k, Sp), vp = pad_seq(v, Sp);
     at::Tensor o = at::empty({B, Sp, Hq, D}, q.options());
@@ -699,6 +700,7 @@ void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, con
   // optional RoPE table [>= S, D/2, 2] fp32 (cos, sin): dq / dk are stored with the inverse rotation
   const float* rtab = nullptr;
   if (rope_tab.has_value()) {
+    TORCH_CHECK(ty != at::kFloat, "attention: the fp32 backward has no fused inverse RoPE (pass rope_tab=None)");
     const at::Tensor& tb = *rope_tab;
     TORCH_CHECK(tb.scalar_type() == at::kFloat && tb.is_contiguous() && tb.numel() >= S * D &&
                     tb.numel() % D == 0, "attention: rope table must be contiguous fp32 [>= S, D/2, 2]");

@@ -29,6 +29,7 @@
 // bwd 0.645 ms (530 TF at the 2.5x-forward convention); B16 H64/8 non-causal fwd 835 TF.
 // B1 S8192 H32/8 causal: bwd 2.68 -> 1.91 ms with the pipelined kernels (719 TF model, 1.0 PF executed).
 #include "common.h"
+#include "launchers.h"
 
 #include <type_traits>
 
@@ -786,7 +787,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
 // the MFMAs of the other -- instead of two waves per SIMD alternating MFMA and VALU phases in
 // lockstep between barriers (bwd_dkdv_kernel):
 //   [S,dP of A] -> [S,dP of B | softmax A] -> [dV,dK += A | softmax B] -> [dV,dK += B]
-// K/V of the block stay in LDS (64 KB at D = 128). Q/dO steps (32 KB) and their per-query
+// K/V of the block land in LDS (64 KB at D = 128) and each wave keeps its own rows' fragments in
+// registers from then on. Q/dO steps (32 KB) and their per-query
 // constants (lse*log2e, delta) arrive by LDS-DMA into a double buffer, issued one step ahead.
 // ======================================================================================
 template <typename T, int D, bool CAUSAL>
@@ -847,6 +849,15 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
 #pragma unroll
   for (int i = 0; i < NDB; ++i) { dkt[i] = f32x16{}; dvt[i] = f32x16{}; }
   __syncthreads();  // K/V and step 0 have landed
+  // the wave's K and V row fragments (B operands of S and dP, the same for every step) are read
+  // from LDS once and kept in registers (B1 S8192 H32/8 dK/dV+dQ 1.871 -> 1.851 ms,
+  // profiles/r3/attn_ab_kvreg.log)
+  V8<T> kf[NKS], vf[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    kf[ks] = lo.rowk(Kw, 0, ks);
+    vf[ks] = lo.rowk(Vw, 0, ks);
+  }
 
   for (int it = 0; it < total; ++it) {
     const int cur = it & 1;
@@ -878,9 +889,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
         if (k < 2 * R1) {
           const int ks = k % R1, r0 = 32 * (k / R1);
           o[0] = lo.rowk(Qs, r0, ks);
-          o[1] = lo.rowk(Kw, 0, ks);
           o[2] = lo.rowk(Ds, r0, ks);
-          o[3] = lo.rowk(Vw, 0, ks);
+          o[1] = kf[ks];
+          o[3] = vf[ks];
         } else if (k < NR) {
           const int st = (k - 2 * R1) % R3, s2 = st / NDB, db = st % NDB, r0 = 32 * ((k - 2 * R1) / R3);
           o[0] = lo.tr(Ds, r0 + 16 * s2, db);
@@ -1291,6 +1302,9 @@ hipError_t pra_attn_fwd(int dtype, const void* q, const void* k, const void* v, 
                         int Hq, int Hkv, int D, long ldq, long ldk, long ldv, long ldo, float scale, int causal,
                         int skv, hipStream_t st) {
   if (skv <= 0 || skv > S) return hipErrorInvalidValue;
+  if (dtype == pra::kF32)
+    return pra_attn_fwd_f32((const float*)q, (const float*)k, (const float*)v, (float*)o, lse, B, S, Hq, Hkv, D, ldq,
+                            ldk, ldv, ldo, scale, causal, skv, st);
   if (dtype == pra::kBF16)
     return attn_fwd_t<__bf16>(q, k, v, o, lse, B, S, Hq, Hkv, D, ldq, ldk, ldv, ldo, scale, causal, skv, st);
   if (dtype == pra::kF16)
@@ -1303,6 +1317,12 @@ hipError_t pra_attn_bwd(int dtype, const void* q, const void* k, const void* v, 
                         int D, long ldq, long ldk, long ldv, long ldo, long lddo, long lddq, long lddk, long lddv,
                         float scale, int causal, int skv, const float* rope_tab, hipStream_t st) {
   if (skv <= 0 || skv > S) return hipErrorInvalidValue;
+  if (dtype == pra::kF32) {
+    if (rope_tab != nullptr) return hipErrorInvalidValue;  // the fp32 kernels have no fused inverse RoPE
+    return pra_attn_bwd_f32((const float*)q, (const float*)k, (const float*)v, (const float*)o, (const float*)dout,
+                            lse, delta, (float*)dq, (float*)dk, (float*)dv, B, S, Hq, Hkv, D, ldq, ldk, ldv, ldo, lddo,
+                            lddq, lddk, lddv, scale, causal, skv, st);
+  }
   if (dtype == pra::kBF16)
     return attn_bwd_t<__bf16>(q, k, v, o, dout, lse, delta, dq, dk, dv, B, S, Hq, Hkv, D, ldq, ldk, ldv, ldo, lddo,
                               lddq, lddk, lddv, scale, causal, skv, rope_tab, st);

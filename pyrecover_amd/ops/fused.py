@@ -385,15 +385,17 @@ def add_layer_norm(x, delta, weight, bias, slot, eps):
 
 # ---------------------------------------------------------------------------------------
 def _attn_hip(q, k):
-    """The MFMA kernels: bf16/fp16, head_dim 64 or 128, whole GQA groups, 16-B aligned rows."""
-    return (_ext.hip16(q) and q.shape[-1] in (64, 128) and q.shape[2] % k.shape[2] == 0
+    """The MFMA kernels: bf16/fp16 (attention.hip) or fp32 (attention_f32.hip, f32-input MFMA),
+    head_dim 64 or 128, whole GQA groups, 16-B aligned rows."""
+    return (_ext.hip(q) and q.shape[-1] in (64, 128) and q.shape[2] % k.shape[2] == 0
             and all(t.stride(-1) == 1 and t.stride(1) % 8 == 0 for t in (q, k)))
 
 
 def _attn_fwd(q, k, v, scale, causal):
-    """HIP flash attention for bf16/fp16 GPU tensors with head_dim 64/128 (any S: the binding
-    zero-pads sequences that do not tile); otherwise torch SDPA in fp32 (fp64 for fp64 inputs),
-    as the reference's non-flash path (reference model.py:192, 227). Returns (o, lse or None)."""
+    """HIP flash attention for bf16/fp16/fp32 GPU tensors with head_dim 64/128 (any S: the binding
+    zero-pads sequences that do not tile); otherwise (fp64, other head dims) torch math in the
+    input's precision, as the reference's non-flash path (reference model.py:192, 227).
+    Returns (o, lse or None)."""
     if _attn_hip(q, k):
         return _ext.require_for(q).attn_fwd(q, k, v, scale, causal)
     ct = torch.promote_types(q.dtype, torch.float32)
@@ -407,6 +409,8 @@ def _attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, causal, rope_tab=None) -> 
     store dq and dk with the inverse rotation already applied; returns whether that happened (the
     torch path leaves it to the caller)."""
     if lse is not None and _attn_hip(q, k):
+        if q.dtype == torch.float32:
+            rope_tab = None  # the fp32 kernels have no fused inverse RoPE: the caller applies it
         _ext.require_for(q).attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, causal, rope_tab)
         return rope_tab is not None
     ct = torch.promote_types(q.dtype, torch.float32)

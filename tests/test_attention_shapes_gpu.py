@@ -1,6 +1,7 @@
 """Attention coverage beyond the tiled bf16 fast path, against fp32 oracles:
 
 * fp16 instantiations of every kernel (v_mfma_f32_32x32x16_f16);
+* the fp32 kernels (attention_f32.hip, v_mfma_f32_32x32x2_f32) for fp32 models;
 * sequence lengths that do not tile (S % 64 / S % 128 != 0): zero-padded in the binding, exact for
   causal attention and key-bounded (skv) for full attention;
 * the production shapes with the DEFAULT kernel selection (no env overrides): Llama-2-7B layer
@@ -99,12 +100,29 @@ def test_production_shapes_default_kernels(cuda, attn_opts, B, S, Hq, Hkv):
     assert torch.equal(dq, dq2) and torch.equal(dk, dk2) and torch.equal(dv, dv2)
 
 
-def test_flash_attention_op_fp32_and_fp64_use_torch_math(cuda):
-    """fp32/fp64 GPU tensors take the SDPA path (the MFMA kernels are 16-bit) with autograd."""
+@pytest.mark.parametrize("B,S,Hq,Hkv,D", [(2, 256, 4, 4, 128), (1, 512, 8, 2, 128), (1, 384, 4, 1, 64),
+                                         (2, 1000, 4, 2, 128), (1, 130, 2, 1, 64), (2, 1, 4, 2, 128)])
+@pytest.mark.parametrize("causal", [True, False])
+def test_fp32_attention_fwd_bwd(cuda, B, S, Hq, Hkv, D, causal):
+    """fp32 kernels (attention_f32.hip, v_mfma_f32_32x32x2_f32) against the fp32 oracle, incl.
+    untiled lengths (zero-padded to 128 in the binding) and GQA; the backward is bit-reproducible."""
+    q, k, v, o, lse, do, dq, dk, dv = _run(cuda, B, S, Hq, Hkv, D, causal, torch.float32, seed=S + D, tol=1e-4)
+    dq2, dk2, dv2 = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    _ext.native().attn_bwd(q, k, v, o, do, lse, dq2, dk2, dv2, 1 / math.sqrt(D), causal)
+    assert torch.equal(dq, dq2) and torch.equal(dk, dk2) and torch.equal(dv, dv2)
+
+
+def test_flash_attention_op_fp32_hip_and_fp64_torch(cuda):
+    """The autograd op: fp32 GPU tensors run the fp32 HIP kernels, fp64 the torch math."""
     for dt in (torch.float32, torch.float64):
         q, k, v = (t.clone().requires_grad_() for t in _qkv(cuda, 1, 100, 4, 2, 64, dt))
         o = F.flash_attention(q, k, v, causal=True)
         o.sum().backward()
         assert o.dtype == dt and q.grad.dtype == dt
-        ref = R.attention_ref(q.detach().double(), k.detach().double(), v.detach().double(), True)
-        assert _rel(o.double(), ref) < (1e-5 if dt == torch.float32 else 1e-10)
+        qd, kd, vd = (t.detach().double().requires_grad_() for t in (q, k, v))
+        ref = R.attention_ref(qd, kd, vd, True)
+        ref.sum().backward()
+        tol = 1e-5 if dt == torch.float32 else 1e-10
+        assert _rel(o.double(), ref) < tol
+        for got, want in ((q.grad, qd.grad), (k.grad, kd.grad), (v.grad, vd.grad)):
+            assert _rel(got.double(), want) < 10 * tol

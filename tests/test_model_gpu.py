@@ -41,7 +41,8 @@ def ref_forward(m, tok):
     ("llama-micro", {}, torch.float64, "auto")])
 def test_model_grads_vs_fp32_reference(cuda, monkeypatch, preset, over, dtype, kernels):
     """Every --model-dtype trains on the GPU: bf16/fp16 on the HIP kernels, fp32 on the HIP
-    element-wise kernels + torch attention, fp64 on torch math (reference utils.py:11-16).
+    element-wise and fp32 attention kernels (GEMMs on the library), fp64 on torch math
+    (reference utils.py:11-16).
     kernels="mfma" forces every GEMM site onto the hand-written MFMA GEMMs, "lib" onto hipBLASLt."""
     from pyrecover_amd.ops import fused
 

@@ -25,12 +25,18 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def parse_arm(spec):
+    """`opt.ATTR=value` sets an attribute of the optimizer instance; the item `noupdate` skips the
+    AdamW update kernels (a diagnostic arm: what the optimizer costs the step)."""
     name, _, body = spec.partition(":")
     sets = []
     for item in filter(None, body.split(";")):
+        if item.strip() == "noupdate":
+            sets.append(("opt", "_update_range", "noupdate"))
+            continue
         lhs, _, rhs = item.partition("=")
         mod, _, attr = lhs.strip().rpartition(".")
-        sets.append((importlib.import_module("pyrecover_amd." + mod), attr, ast.literal_eval(rhs.strip())))
+        target = "opt" if mod == "opt" else importlib.import_module("pyrecover_amd." + mod)
+        sets.append((target, attr, ast.literal_eval(rhs.strip())))
     return name, sets
 
 
@@ -79,9 +85,18 @@ def main():
         opt.step()
         return loss
 
+    def resolve(sets):
+        out = []
+        for m, k, v in sets:
+            m = opt if m == "opt" else m
+            if v == "noupdate":
+                v = lambda *args, **kw: None  # noqa: E731
+            out.append((m, k, v))
+        return out
+
     def run(arm, n):
-        _, sets = arm
-        old = [(m, k, getattr(m, k)) for m, k, _ in sets]
+        sets = resolve(arm[1])
+        old = [(m, k, m.__dict__[k] if k in m.__dict__ else getattr(m, k)) for m, k, _ in sets]
         for m, k, v in sets:
             setattr(m, k, v)
         try:
@@ -93,7 +108,10 @@ def main():
             return (time.perf_counter() - t0) * 1000 / n, float(loss.item())
         finally:
             for m, k, v in old:
-                setattr(m, k, v)
+                if m is opt and k == "_update_range":
+                    del m.__dict__[k]  # back to the class method
+                else:
+                    setattr(m, k, v)
 
     for arm in arms:
         run(arm, a.warmup)
