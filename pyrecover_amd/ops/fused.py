@@ -140,14 +140,27 @@ WGRAD_AUTO = os.environ.get("PYRECOVER_WGRAD", "auto") == "auto"
 WGRAD_AUTO_MIN_TOKENS = 16384
 
 
+def _wgrad_fills_chip(t, cols) -> bool:
+    """auto: at least one 256 x 256 output tile per CU. Smaller outputs (GPT-2-medium's 16 / 48 / 88
+    tiles) leave most CUs idle on the kernel, which splits only a partial LAST round over K; there
+    hipBLASLt's K-split on transposed copies is 1.5-3x faster (profiles/r3/wgrad_bench_gpt2m_*.log:
+    QKV 3072x1024x32768 565 vs 321 us, O 574 vs 154 us, W1|W3 596 vs 464 us; step 123.9 -> 103.2 ms)."""
+    tiles = 1
+    for c in cols:
+        tiles *= c // 256
+    return tiles >= _cus(t)
+
+
 def _hip_wgrad_dims(t, site, tokens, *cols, force=False) -> bool:
     """The MFMA weight-gradient kernel's shape rules: K = tokens % 32, every output dim % 256.
     `force`: the operands exist only row-major (no transposed copy to hand the library), so the
     kernel runs whatever the site list and token threshold say (PYRECOVER_WGRAD=lib still wins)."""
     if WGRAD_SITES == _WGRAD_SITE_SETS["lib"] and os.environ.get("PYRECOVER_WGRAD") == "lib":
         force = False
-    return ((force or (site in WGRAD_SITES and (not WGRAD_AUTO or tokens >= WGRAD_AUTO_MIN_TOKENS)))
-            and _ext.hip16(t) and tokens % 32 == 0 and tokens > 0 and all(c % 256 == 0 for c in cols))
+    if not (_ext.hip16(t) and tokens % 32 == 0 and tokens > 0 and all(c % 256 == 0 for c in cols)):
+        return False
+    return force or (site in WGRAD_SITES and (not WGRAD_AUTO or (tokens >= WGRAD_AUTO_MIN_TOKENS
+                                                                 and _wgrad_fills_chip(t, cols))))
 
 
 def _hip_wgrad_ok(dy2, x2, site, force=False) -> bool:

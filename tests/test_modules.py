@@ -101,3 +101,18 @@ def test_wgrad_site_selection_parsing():
         fused._wgrad_sites("o,attn")
     x = torch.zeros(32768, 256, dtype=torch.bfloat16)
     assert not fused._hip_wgrad_ok(x, x, "o")
+
+
+def test_wgrad_auto_needs_one_tile_per_cu(monkeypatch):
+    """auto mode sends weight gradients with fewer 256 x 256 output tiles than CUs (GPT-2-medium)
+    to the library; the 7B shapes keep the MFMA kernel."""
+    import torch
+
+    from pyrecover_amd.ops import fused
+
+    monkeypatch.setattr(fused, "_cus", lambda t: 256)
+    t = torch.zeros(1)
+    assert not fused._wgrad_fills_chip(t, (3072, 1024))  # GPT-2-medium QKV: 48 tiles
+    assert not fused._wgrad_fills_chip(t, (5632, 1024))  # GPT-2-medium W1|W3: 88 tiles
+    assert fused._wgrad_fills_chip(t, (4096, 4096))  # 7B O: 256 tiles
+    assert fused._wgrad_fills_chip(t, (22016, 4096))  # 7B W1|W3: 1376 tiles

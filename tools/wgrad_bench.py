@@ -30,7 +30,12 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--shapes", default="")
+    ap.add_argument("--dims", default="", help="name:M:N[,...] instead of the 7B shapes (e.g. GPT-2-medium "
+                    "qkv:3072:1024,o:1024:1024,w13:5632:1024)")
     args = ap.parse_args()
+    global SHAPES
+    if args.dims:
+        SHAPES = [(n, int(m), int(k)) for n, m, k in (d.split(":") for d in args.dims.split(","))]
     from pyrecover_amd.utils.gemm_tuning import configure_gemm_tuning
 
     configure_gemm_tuning("auto")  # the library arms use the step's tuned solution table
