@@ -67,8 +67,9 @@ __device__ __forceinline__ void load_half(float (&x)[D / 2], const float* row, i
   }
 }
 
-// acc (+)= Rows(tile rows r0 .. r0+31, lane row l32) . x over d (x = the other operand's half-row)
-template <int D, bool ROWS_A>
+// acc (+)= Rows x^T over d: A = the LDS tile's rows r0 .. r0+31 (lane row l32), B = x, the lane's
+// half-row of the other operand (the accumulator's column index is x's row)
+template <int D>
 __device__ __forceinline__ f32x16 dot_rows(f32x16 acc, const float* tile, int r0, int l32, int h2,
                                            const float (&x)[D / 2]) {
   const float* p = tile + (r0 + l32) * (D + 4) + (D / 2) * h2;
@@ -77,7 +78,7 @@ __device__ __forceinline__ f32x16 dot_rows(f32x16 acc, const float* tile, int r0
     const float4 t = *reinterpret_cast<const float4*>(p + 4 * j);
     const float tv[4] = {t.x, t.y, t.z, t.w};
 #pragma unroll
-    for (int e = 0; e < 4; ++e) acc = ROWS_A ? mfma2(tv[e], x[4 * j + e], acc) : mfma2(x[4 * j + e], tv[e], acc);
+    for (int e = 0; e < 4; ++e) acc = mfma2(tv[e], x[4 * j + e], acc);
   }
   return acc;
 }
@@ -130,7 +131,7 @@ __global__ __launch_bounds__(256, 1) void fwd_kernel(const float* __restrict__ Q
     f32x16 s[2];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
-      s[kb] = dot_rows<D, true>(f32x16{}, Ks, 32 * kb, l32, h2, qr);  // S^T = K Q^T
+      s[kb] = dot_rows<D>(f32x16{}, Ks, 32 * kb, l32, h2, qr);  // S^T = K Q^T
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int key = k0 + 32 * kb + crow(r, h2);
@@ -217,8 +218,8 @@ __global__ __launch_bounds__(256, 1) void bwd_dq_kernel(const float* __restrict_
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
       if (CAUSAL && k0 + 32 * kb > qw + 31) continue;
-      f32x16 s = dot_rows<D, true>(f32x16{}, Ks, 32 * kb, l32, h2, qr);
-      f32x16 dp = dot_rows<D, true>(f32x16{}, Vs, 32 * kb, l32, h2, dr);
+      f32x16 s = dot_rows<D>(f32x16{}, Ks, 32 * kb, l32, h2, qr);
+      f32x16 dp = dot_rows<D>(f32x16{}, Vs, 32 * kb, l32, h2, dr);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int key = k0 + 32 * kb + crow(r, h2);
@@ -278,8 +279,8 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(
       }
       __syncthreads();
       if (CAUSAL && q0 + QT - 1 < kw) continue;  // wave-uniform: every query precedes the wave's keys
-      f32x16 s = dot_rows<D, true>(f32x16{}, Qs, 0, l32, h2, kr);   // A = Q rows, B = K^T
-      f32x16 dp = dot_rows<D, true>(f32x16{}, Ds, 0, l32, h2, vr);  // A = dO rows, B = V^T
+      f32x16 s = dot_rows<D>(f32x16{}, Qs, 0, l32, h2, kr);   // A = Q rows, B = K^T
+      f32x16 dp = dot_rows<D>(f32x16{}, Ds, 0, l32, h2, vr);  // A = dO rows, B = V^T
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int qi = crow(r, h2);
