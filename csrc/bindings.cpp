@@ -716,7 +716,7 @@ void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, con
     at::Tensor lp = at::zeros({B, Hq, Sp}, lse.options());
     lp.narrow(2, 0, S).copy_(lse.view({B, Hq, S}));
     at::Tensor dqp = at::empty_like(qp), dkp = at::empty_like(kp), dvp = at::empty_like(vp);
-    at::Tensor delta = at::empty({B, Hq, Sp}, q.options().dtype(at::kFloat));
+    at::Tensor delta = at::empty({3, B, Hq, Sp}, q.options().dtype(at::kFloat));  // see pra_attn_bwd
     check(pra_attn_bwd(dt(q), qp.data_ptr(), kp.data_ptr(), vp.data_ptr(), op.data_ptr(), dop.data_ptr(),
                        lp.data_ptr<float>(), delta.data_ptr<float>(), dqp.data_ptr(), dkp.data_ptr(), dvp.data_ptr(),
                        (int)B, (int)Sp, (int)Hq, (int)Hkv, (int)D, qp.stride(1), kp.stride(1), vp.stride(1),
@@ -728,7 +728,7 @@ void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, con
     dv.copy_(dvp.narrow(1, 0, S));
     return;
   }
-  at::Tensor delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
+  at::Tensor delta = at::empty({3, B, Hq, S}, q.options().dtype(at::kFloat));  // see pra_attn_bwd
   check(pra_attn_bwd(dt(q), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
                      lse.data_ptr<float>(), delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
                      (int)B, (int)S, (int)Hq, (int)Hkv, (int)D, q.stride(1), k.stride(1), v.stride(1), o.stride(1),

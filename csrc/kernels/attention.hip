@@ -788,19 +788,23 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
 // lockstep between barriers (bwd_dkdv_kernel):
 //   [S,dP of A] -> [S,dP of B | softmax A] -> [dV,dK += A | softmax B] -> [dV,dK += B]
 // K/V of the block land in LDS (64 KB at D = 128) and each wave keeps its own rows' fragments in
-// registers from then on. Q/dO steps (32 KB) and their per-query
-// constants (lse*log2e, delta) arrive by LDS-DMA into a double buffer, issued one step ahead.
+// registers from then on. Q/dO steps (32 KB) and their per-query constants arrive by LDS-DMA into a
+// double buffer, issued one step ahead. The constants are -lse/scale and -delta, written by the dQ
+// kernel (RC2), and they are the INITIAL values of the S and dP accumulators: S' = Q K^T - lse/scale
+// and dP' = dO V^T - delta leave the MFMA chains ready, so each score needs exp2(c S') and
+// dS = P dP' (2 VALU fewer per element than exp2(fma(S, c, -lse log2e)) and P (dP - delta) in this
+// VALU-bound one-wave kernel).
 // ======================================================================================
 template <typename T, int D, bool CAUSAL>
 __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
     const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V,
-    const T* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
+    const T* __restrict__ dO, const float* __restrict__ NLS, const float* __restrict__ NDelta,
     T* __restrict__ dK, T* __restrict__ dV, int S, int Hq, int Hkv, long ldq, long ldk, long ldv,
     long lddo, long lddk, long lddv, float scale, float scale_log2, int skv, const float2* __restrict__ rtab) {
   constexpr int NW = 4, KB = 32 * NW, QS = 64;
   constexpr int NKS = D / 16, NDB = D / 32;
   constexpr int KVT = KB * D, QDT = QS * D;
-  // Q0 dO0 Q1 dO1 (steps, double-buffered) | K V | row constants [buf][lse, delta][64]
+  // Q0 dO0 Q1 dO1 (steps, double-buffered) | K V | row constants [buf][-lse/scale, -delta][64]
   __shared__ __attribute__((aligned(16))) T smem[4 * QDT + 2 * KVT];
   __shared__ __attribute__((aligned(16))) float rowc[2][2][QS];
   T* const Ks = smem + 4 * QDT;
@@ -826,8 +830,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
     const int q0 = qstart + (t % nqs) * QS;
     gq.issue(Q + ((long)b * S + q0) * ldq + hq * D, smem + buf * 2 * QDT);
     gd.issue(dO + ((long)b * S + q0) * lddo + hq * D, smem + buf * 2 * QDT + QDT);
-    if (wid < 2) {  // wave 0: lse, wave 1: delta (one dword per lane)
-      const float* src = (wid ? Delta : LSE) + ((long)b * Hq + hq) * S + q0 + lane;
+    if (wid < 2) {  // wave 0: -lse/scale, wave 1: -delta (one dword per lane)
+      const float* src = (wid ? NDelta : NLS) + ((long)b * Hq + hq) * S + q0 + lane;
       __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)&rowc[buf][wid][0], 4, 0, 0);
     }
@@ -882,9 +886,18 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
       constexpr int R1 = NKS, R3 = 2 * NDB, NR = 2 * R1 + 2 * R3;
       constexpr int EA = 16 / R1, EB = 16 / R3;  // softmax rows per region
       const int lim = kw + l32 - q0 - 4 * h2;
-      f32x16 sa = f32x16{}, sb = f32x16{}, pa = f32x16{}, pb = f32x16{};
+      // accumulators start at the row constants of their query rows (register r: row crow(r, h2))
+      auto rc16 = [&](const float* row) {
+        f32x16 a;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const f32x4 c = *reinterpret_cast<const f32x4*>(row + 8 * rr + 4 * h2);
+          a[4 * rr] = c[0]; a[4 * rr + 1] = c[1]; a[4 * rr + 2] = c[2]; a[4 * rr + 3] = c[3];
+        }
+        return a;
+      };
+      f32x16 sa = rc16(lrow), sb = rc16(lrow + 32), pa = rc16(drow), pb = rc16(drow + 32);
       V8<T> pA[2], gA[2], pB[2], gB[2];
-      f32x4 lc[4], dc[4];  // row constants of the sub-tile being softmaxed
       auto fetch = [&](int k, V8<T> (&o)[4]) {
         if (k < 2 * R1) {
           const int ks = k % R1, r0 = 32 * (k / R1);
@@ -898,23 +911,15 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
           o[1] = lo.tr(Qs, r0 + 16 * s2, db);
         }
       };
-      auto load_rc = [&](int u) {
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          lc[rr] = *reinterpret_cast<const f32x4*>(lrow + 32 * u + 8 * rr + 4 * h2);
-          dc[rr] = *reinterpret_cast<const f32x4*>(drow + 32 * u + 8 * rr + 4 * h2);
-        }
-      };
       auto soft = [&](f32x16& sv, f32x16& dp, int u, int r) {
-        float p = fexp2(fmaf(sv[r], scale_log2, -lc[r >> 2][r & 3] * 1.4426950408889634f));
+        float p = fexp2(sv[r] * scale_log2);  // sv = S - lse/scale
         if (MASK && crow(r, 0) < lim - 32 * u) p = 0.f;
         if (!CAUSAL && kw + l32 >= skv) p = 0.f;  // padded key
         sv[r] = p;
-        dp[r] = p * (dp[r] - dc[r >> 2][r & 3]);
+        dp[r] = p * dp[r];  // dp = dP - delta
       };
       V8<T> cur[4], nxt[4];
       fetch(0, cur);
-      load_rc(0);
 #pragma unroll
       for (int k = 0; k < NR; ++k) {
         fetch(k + 1, nxt);
@@ -928,7 +933,6 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
           for (int e = 0; e < EA; ++e) soft(sa, pa, 0, (k - R1) * EA + e);
           if (k == 2 * R1 - 1) {
             pA[0] = pack8<T>(sa, 0); pA[1] = pack8<T>(sa, 1); gA[0] = pack8<T>(pa, 0); gA[1] = pack8<T>(pa, 1);
-            load_rc(1);
           }
         } else {
           const int j = k - 2 * R1, st = j % R3, s2 = st / NDB, db = st % NDB;
@@ -975,7 +979,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
     const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V,
     const T* __restrict__ dO, const T* __restrict__ O, const float* __restrict__ LSE, float* __restrict__ Delta,
     T* __restrict__ dQ, int S, int Hq, int Hkv, long ldq, long ldk, long ldv, long lddo, long ldo, long lddq,
-    float scale, float scale_log2, int skv, const float2* __restrict__ rtab) {
+    float scale, float scale_log2, int skv, const float2* __restrict__ rtab, float* __restrict__ RC2, long nrc) {
   constexpr int KT = 64, QT = 32 * NW;
   constexpr int NKS = D / 16, NDB = D / 32, TILE = KT * D;
   // K0 V0 | K1 V1: one __shared__ object per buffer, so the reads of one buffer do not wait
@@ -1030,7 +1034,14 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
       }
     }
     dl = half_sum(part);  // all 64 lanes (permlane32 swap)
-    if (qrow < S && h2 == 0) Delta[((long)b * Hq + hq) * S + qrow] = dl;
+    if (qrow < S && h2 == 0) {
+      const long i = ((long)b * Hq + hq) * S + qrow;
+      Delta[i] = dl;
+      if (RC2 != nullptr) {  // row constants of the pipelined dK/dV kernel: -lse/scale, -delta
+        RC2[i] = -lse2 / scale_log2;
+        RC2[nrc + i] = -dl;
+      }
+    }
   }
 
   f32x16 dqt[NDB];
@@ -1244,6 +1255,11 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
   const float sl2 = scale * 1.4426950408889634f;
   // 8-wave (256-row) blocks; S % 256 != 0 (S % 128 == 0) takes the 4-wave instantiations
   const int nw = S % 256 ? 4 : 8;
+  // delta: fp32 workspace [3][B * Hq * S]: delta, then the pipelined dK/dV kernel's row constants
+  // (-lse/scale, -delta), written by the dQ kernel only when that kernel runs
+  const long nrc = (long)B * Hq * S;
+  const bool p2 = dkdv_use_p2(B, S, Hq, Hkv, D);
+  float* rc2 = p2 ? delta + nrc : nullptr;
   // dQ first: it also computes delta = rowsum(dO * O), which the dK/dV kernel reads
   {
     dim3 grid((S / (32 * nw)) * Hq * B);
@@ -1253,11 +1269,11 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
   if (pipe)                                                                                                     \
     hipLaunchKernelGGL((bwd_dq_kernel<T, DD, CC, NWW, true>), grid, dim3(NWW * 64), 0, st, (const T*)q,       \
                        (const T*)k, (const T*)v, (const T*)dout, (const T*)o, lse, delta, (T*)dq, S, Hq, Hkv,  \
-                       ldq, ldk, ldv, lddo, ldo, lddq, scale, sl2, skv, rt);                                        \
+                       ldq, ldk, ldv, lddo, ldo, lddq, scale, sl2, skv, rt, rc2, nrc);                              \
   else                                                                                                          \
     hipLaunchKernelGGL((bwd_dq_kernel<T, DD, CC, NWW>), grid, dim3(NWW * 64), 0, st, (const T*)q,             \
                        (const T*)k, (const T*)v, (const T*)dout, (const T*)o, lse, delta, (T*)dq, S, Hq, Hkv,  \
-                       ldq, ldk, ldv, lddo, ldo, lddq, scale, sl2, skv, rt)
+                       ldq, ldk, ldv, lddo, ldo, lddq, scale, sl2, skv, rt, rc2, nrc)
     if (nw == 8) {
       if (D == 128) { if (causal) LAUNCH(128, true, 8); else LAUNCH(128, false, 8); }
       else { if (causal) LAUNCH(64, true, 8); else LAUNCH(64, false, 8); }
@@ -1267,12 +1283,12 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
     }
 #undef LAUNCH
   }
-  if (dkdv_use_p2(B, S, Hq, Hkv, D)) {
+  if (p2) {
     dim3 g1((S / 128) * Hkv * B);
 #define LAUNCH1(DD, CC)                                                                                       \
   hipLaunchKernelGGL((bwd_dkdv_p2_kernel<T, DD, CC>), g1, dim3(256), 0, st, (const T*)q, (const T*)k,        \
-                     (const T*)v, (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Hq, Hkv, ldq, ldk, ldv, lddo, \
-                     lddk, lddv, scale, sl2, skv, rt)
+                     (const T*)v, (const T*)dout, rc2, rc2 + nrc, (T*)dk, (T*)dv, S, Hq, Hkv, ldq, ldk, ldv,   \
+                     lddo, lddk, lddv, scale, sl2, skv, rt)
     if (D == 128) { if (causal) LAUNCH1(128, true); else LAUNCH1(128, false); }
     else { if (causal) LAUNCH1(64, true); else LAUNCH1(64, false); }
 #undef LAUNCH1

@@ -74,6 +74,7 @@ hipError_t pra_adamw_t(int dtype, void* p, const void* g, void* m, void* v, void
 hipError_t pra_attn_fwd(int dtype, const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int Hq,
                         int Hkv, int D, long ldq, long ldk, long ldv, long ldo, float scale, int causal,
                         int skv, hipStream_t st);
+// delta: fp32 workspace of 3 * B * Hq * S floats (delta and the pipelined dK/dV kernel's row constants)
 hipError_t pra_attn_bwd(int dtype, const void* q, const void* k, const void* v, const void* o, const void* dout,
                         const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int S, int Hq, int Hkv,
                         int D, long ldq, long ldk, long ldv, long ldo, long lddo, long lddq, long lddk, long lddv,
