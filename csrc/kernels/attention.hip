@@ -681,8 +681,9 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
   const int qstart = CAUSAL ? k0 : 0;
   const int nqt = (S - qstart) / QT;
   const int total = nqt * nrep;
-  // lane reads the row constant of query row l32 of the tile: lse*log2e (h2 = 0) or delta (h2 = 1)
-  const float rc_mul = h2 ? 1.f : 1.4426950408889634f;
+  // lane reads the row constant of query row l32 of the tile: lse*log2e (h2 = 0) or delta (h2 = 1);
+  // NW = 8 stages them negated: they are the S / dP accumulators' initial values (below)
+  const float rc_mul = ROWC_LDS ? (h2 ? -1.f : -1.4426950408889634f) : (h2 ? 1.f : 1.4426950408889634f);
   const float* rc_base = (h2 ? Delta : LSE) + (long)b * Hq * S + l32;
   int bp_base = 4 * (4 * h2);  // ds_bpermute byte address of lane crow(0, h2)
   asm volatile("" : "+v"(bp_base));  // opaque: per-row offsets then fold into the ds offset field
@@ -697,6 +698,21 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
     if (ROWC_LDS && wid == 0) rc_next = rc_base[(long)hq * S + q0] * rc_mul;
   };
   if (total > 0) stage_load(0);
+  if constexpr (ROWC_LDS) {
+    // K pre-multiplied by c = scale * log2(e) in LDS, once per block (one extra rounding of K to T):
+    // each wave rescales its own 32 contiguous rows (8 KiB of the image), which only it reads
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    char* kb = reinterpret_cast<char*>(Ks) + wid * 32 * D * (int)sizeof(T);
+#pragma unroll
+    for (int i = 0; i < 32 * D * (int)sizeof(T) / 1024; ++i) {
+      V8<T>& c8 = *reinterpret_cast<V8<T>*>(kb + i * 1024 + lane * 16);
+      V8<T> v8 = c8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v8[j] = (T)((float)v8[j] * scale_log2);
+      c8 = v8;
+    }
+  }
 
   for (int it = 0; it < total; ++it) {
     const int hq = hk * nrep + it / nqt;
@@ -712,7 +728,25 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
     __syncthreads();
     if (it + 1 < total) stage_load(it + 1);
     if (!(CAUSAL && q0 + QT - 1 < kw)) {
+      const bool diag = CAUSAL && q0 == kw;
       f32x16 s = f32x16{}, dp = f32x16{};
+      if constexpr (ROWC_LDS) {
+        // S' = (c K) Q^T - lse log2(e), dP' = dO V^T - delta: the accumulators start at the
+        // (negated) row constants of their query rows crow(r, h2); on the diagonal tile the causal
+        // mask rides on the S initial values (-inf)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const float4 a = *reinterpret_cast<const float4*>(&rowc[0][8 * rr + 4 * h2]);
+          const float4 c = *reinterpret_cast<const float4*>(&rowc[1][8 * rr + 4 * h2]);
+          s[4 * rr] = a.x; s[4 * rr + 1] = a.y; s[4 * rr + 2] = a.z; s[4 * rr + 3] = a.w;
+          dp[4 * rr] = c.x; dp[4 * rr + 1] = c.y; dp[4 * rr + 2] = c.z; dp[4 * rr + 3] = c.w;
+        }
+        if (diag) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (l32 > crow(r, h2)) s[r] = -INFINITY;
+        }
+      }
       // S chain then dP chain: one operand pair in flight ahead of each MFMA
       V8<T> xa = lo.rowk(Qs, 0, 0), xb = lo.rowk(Kw, 0, 0);
 #pragma unroll
@@ -728,31 +762,33 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
         else dp = mfma(xa, xb, dp);
         xa = na; xb = nb;
       }
-      const bool diag = CAUSAL && q0 == kw;
+      if constexpr (ROWC_LDS) {
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        float lse4[4], dl4[4];
-        if constexpr (ROWC_LDS) {
-          const float4 a = *reinterpret_cast<const float4*>(&rowc[0][8 * rr + 4 * h2]);
-          const float4 c = *reinterpret_cast<const float4*>(&rowc[1][8 * rr + 4 * h2]);
-          lse4[0] = a.x; lse4[1] = a.y; lse4[2] = a.z; lse4[3] = a.w;
-          dl4[0] = c.x; dl4[1] = c.y; dl4[2] = c.z; dl4[3] = c.w;
-        } else {
+        for (int r = 0; r < 16; ++r) {
+          float p = fexp2(s[r]);
+          if (!CAUSAL && krow >= skv) p = 0.f;  // padded key
+          s[r] = p;
+          dp[r] = p * dp[r];
+        }
+      } else {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          float lse4[4], dl4[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int src = bp_base + 4 * (j + 8 * rr);
             lse4[j] = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(rcv)));
             dl4[j] = __int_as_float(__builtin_amdgcn_ds_bpermute(src + 128, __float_as_int(rcv)));
           }
-        }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int r = 4 * rr + j;
-          float p = fexp2(fmaf(s[r], scale_log2, -lse4[j]));
-          if (diag && l32 > crow(r, h2)) p = 0.f;
-          if (!CAUSAL && krow >= skv) p = 0.f;  // padded key
-          s[r] = p;
-          dp[r] = p * (dp[r] - dl4[j]);
+          for (int j = 0; j < 4; ++j) {
+            const int r = 4 * rr + j;
+            float p = fexp2(fmaf(s[r], scale_log2, -lse4[j]));
+            if (diag && l32 > crow(r, h2)) p = 0.f;
+            if (!CAUSAL && krow >= skv) p = 0.f;  // padded key
+            s[r] = p;
+            dp[r] = p * (dp[r] - dl4[j]);
+          }
         }
       }
       const V8<T> p0 = pack8<T>(s, 0), p1 = pack8<T>(s, 1), d0 = pack8<T>(dp, 0), d1 = pack8<T>(dp, 1);
@@ -789,11 +825,12 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
 //   [S,dP of A] -> [S,dP of B | softmax A] -> [dV,dK += A | softmax B] -> [dV,dK += B]
 // K/V of the block land in LDS (64 KB at D = 128) and each wave keeps its own rows' fragments in
 // registers from then on. Q/dO steps (32 KB) and their per-query constants arrive by LDS-DMA into a
-// double buffer, issued one step ahead. The constants are -lse/scale and -delta, written by the dQ
-// kernel (RC2), and they are the INITIAL values of the S and dP accumulators: S' = Q K^T - lse/scale
-// and dP' = dO V^T - delta leave the MFMA chains ready, so each score needs exp2(c S') and
-// dS = P dP' (2 VALU fewer per element than exp2(fma(S, c, -lse log2e)) and P (dP - delta) in this
-// VALU-bound one-wave kernel).
+// double buffer, issued one step ahead. The constants are -lse log2(e) and -delta, written by the dQ
+// kernel (RC2), and they are the INITIAL values of the S and dP accumulators; with K pre-multiplied
+// by c = scale log2(e) and the causal mask folded into the S initial values on diagonal steps,
+// S' = (c K) Q^T - lse log2(e) and dP' = dO V^T - delta leave the MFMA chains ready: each score
+// costs exp2(S') and dS = P dP' (4 VALU fewer per element than exp2(fma(S, c, -lse log2e)), a mask
+// select and P (dP - delta), in this VALU-bound one-wave kernel).
 // ======================================================================================
 template <typename T, int D, bool CAUSAL>
 __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
@@ -804,7 +841,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
   constexpr int NW = 4, KB = 32 * NW, QS = 64;
   constexpr int NKS = D / 16, NDB = D / 32;
   constexpr int KVT = KB * D, QDT = QS * D;
-  // Q0 dO0 Q1 dO1 (steps, double-buffered) | K V | row constants [buf][-lse/scale, -delta][64]
+  // Q0 dO0 Q1 dO1 (steps, double-buffered) | K V | row constants [buf][-lse log2(e), -delta][64]
   __shared__ __attribute__((aligned(16))) T smem[4 * QDT + 2 * KVT];
   __shared__ __attribute__((aligned(16))) float rowc[2][2][QS];
   T* const Ks = smem + 4 * QDT;
@@ -830,7 +867,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
     const int q0 = qstart + (t % nqs) * QS;
     gq.issue(Q + ((long)b * S + q0) * ldq + hq * D, smem + buf * 2 * QDT);
     gd.issue(dO + ((long)b * S + q0) * lddo + hq * D, smem + buf * 2 * QDT + QDT);
-    if (wid < 2) {  // wave 0: -lse/scale, wave 1: -delta (one dword per lane)
+    if (wid < 2) {  // wave 0: -lse log2(e), wave 1: -delta (one dword per lane)
       const float* src = (wid ? NDelta : NLS) + ((long)b * Hq + hq) * S + q0 + lane;
       __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)&rowc[buf][wid][0], 4, 0, 0);
@@ -856,10 +893,14 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
   // the wave's K and V row fragments (B operands of S and dP, the same for every step) are read
   // from LDS once and kept in registers (B1 S8192 H32/8 dK/dV+dQ 1.871 -> 1.851 ms,
   // profiles/r3/attn_ab_kvreg.log)
+  // K is pre-multiplied by c = scale * log2(e) once (one extra rounding of K to T), so S = (c K) Q^T
+  // needs no per-score multiply before its exp2
   V8<T> kf[NKS], vf[NKS];
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) {
     kf[ks] = lo.rowk(Kw, 0, ks);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) kf[ks][j] = (T)((float)kf[ks][j] * scale_log2);
     vf[ks] = lo.rowk(Vw, 0, ks);
   }
 
@@ -897,6 +938,15 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
         return a;
       };
       f32x16 sa = rc16(lrow), sb = rc16(lrow + 32), pa = rc16(drow), pb = rc16(drow + 32);
+      // the causal mask rides on the S initial values (-inf: exp2 gives exactly 0), and only on the
+      // steps that cross the diagonal (wave-uniform), so the softmax itself carries no mask select
+      if (MASK && q0 < kw + 32) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          if (crow(r, 0) < lim) sa[r] = -INFINITY;
+          if (crow(r, 0) < lim - 32) sb[r] = -INFINITY;
+        }
+      }
       V8<T> pA[2], gA[2], pB[2], gB[2];
       auto fetch = [&](int k, V8<T> (&o)[4]) {
         if (k < 2 * R1) {
@@ -912,8 +962,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
         }
       };
       auto soft = [&](f32x16& sv, f32x16& dp, int u, int r) {
-        float p = fexp2(sv[r] * scale_log2);  // sv = S - lse/scale
-        if (MASK && crow(r, 0) < lim - 32 * u) p = 0.f;
+        float p = fexp2(sv[r]);  // sv = (c K) Q^T - lse log2(e), -inf where masked
         if (!CAUSAL && kw + l32 >= skv) p = 0.f;  // padded key
         sv[r] = p;
         dp[r] = p * dp[r];  // dp = dP - delta
@@ -1037,8 +1086,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
     if (qrow < S && h2 == 0) {
       const long i = ((long)b * Hq + hq) * S + qrow;
       Delta[i] = dl;
-      if (RC2 != nullptr) {  // row constants of the pipelined dK/dV kernel: -lse/scale, -delta
-        RC2[i] = -lse2 / scale_log2;
+      if (RC2 != nullptr) {  // row constants of the pipelined dK/dV kernel: -lse log2(e), -delta
+        RC2[i] = -lse2;
         RC2[nrc + i] = -dl;
       }
     }
@@ -1256,7 +1305,7 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
   // 8-wave (256-row) blocks; S % 256 != 0 (S % 128 == 0) takes the 4-wave instantiations
   const int nw = S % 256 ? 4 : 8;
   // delta: fp32 workspace [3][B * Hq * S]: delta, then the pipelined dK/dV kernel's row constants
-  // (-lse/scale, -delta), written by the dQ kernel only when that kernel runs
+  // (-lse log2(e), -delta), written by the dQ kernel only when that kernel runs
   const long nrc = (long)B * Hq * S;
   const bool p2 = dkdv_use_p2(B, S, Hq, Hkv, D);
   float* rc2 = p2 ? delta + nrc : nullptr;
