@@ -679,8 +679,11 @@ std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const
 // Writes dq/dk/dv into caller-provided [B,S,H,D] views (e.g. slices of a fused dQKV buffer).
 void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const at::Tensor& o,
               const at::Tensor& dout, const at::Tensor& lse, at::Tensor dq, at::Tensor dk, at::Tensor dv, double scale,
-              bool causal, c10::optional<at::Tensor> rope_tab) {
+              bool causal, c10::optional<at::Tensor> rope_tab, int64_t mid_event) {
   const Range range_("pyrecover::attn_bwd");
+  // mid_event (optional, a torch.cuda.Event's cuda_event handle): recorded on the stream between the
+  // dQ and dK/dV kernels, so another stream can start work under the dK/dV kernel
+  hipEvent_t mev = reinterpret_cast<hipEvent_t>(mid_event);
   check_dev(q, "q");
   check_attn_dtype(q);
   const int64_t B = q.size(0), S = q.size(1), Hq = q.size(2), D = q.size(3), Hkv = k.size(2);
@@ -721,7 +724,7 @@ void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, con
                        lp.data_ptr<float>(), delta.data_ptr<float>(), dqp.data_ptr(), dkp.data_ptr(), dvp.data_ptr(),
                        (int)B, (int)Sp, (int)Hq, (int)Hkv, (int)D, qp.stride(1), kp.stride(1), vp.stride(1),
                        op.stride(1), dop.stride(1), dqp.stride(1), dkp.stride(1), dvp.stride(1), (float)scale,
-                       causal ? 1 : 0, (int)S, rtab, stream_of(q)),
+                       causal ? 1 : 0, (int)S, rtab, mev, stream_of(q)),
           "attn_bwd");
     dq.copy_(dqp.narrow(1, 0, S));
     dk.copy_(dkp.narrow(1, 0, S));
@@ -733,7 +736,7 @@ void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, con
                      lse.data_ptr<float>(), delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
                      (int)B, (int)S, (int)Hq, (int)Hkv, (int)D, q.stride(1), k.stride(1), v.stride(1), o.stride(1),
                      dout.stride(1), dq.stride(1), dk.stride(1), dv.stride(1), (float)scale, causal ? 1 : 0, (int)S,
-                     rtab, stream_of(q)),
+                     rtab, mev, stream_of(q)),
         "attn_bwd");
 }
 
@@ -778,7 +781,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd, pybind11::arg("q"), pybind11::arg("k"), pybind11::arg("v"), pybind11::arg("o"),
         pybind11::arg("dout"), pybind11::arg("lse"), pybind11::arg("dq"), pybind11::arg("dk"), pybind11::arg("dv"),
-        pybind11::arg("scale"), pybind11::arg("causal"), pybind11::arg("rope_tab") = pybind11::none());
+        pybind11::arg("scale"), pybind11::arg("causal"), pybind11::arg("rope_tab") = pybind11::none(),
+        pybind11::arg("mid_event") = 0);
   m.def("attn_set_options", [](int fwd_pipe, double fwd_thr, int dkdv_impl, int dq_pipe) {
     pra_attn_set_options(fwd_pipe, (float)fwd_thr, dkdv_impl, dq_pipe);
   }, "attention kernel selection: fwd_pipe / dkdv_impl / dq_pipe = -1 (by shape), 0 or 1; fwd_thr = rescale threshold (log2)");

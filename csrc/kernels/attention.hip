@@ -1296,7 +1296,8 @@ template <typename T>
 hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o, const void* dout,
                         const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int S, int Hq, int Hkv,
                         int D, long ldq, long ldk, long ldv, long ldo, long lddo, long lddq, long lddk, long lddv,
-                        float scale, int causal, int skv, const float* rope_tab, hipStream_t st) {
+                        float scale, int causal, int skv, const float* rope_tab, hipEvent_t mid_event,
+                        hipStream_t st) {
   if (S % 128 || (D != 64 && D != 128) || Hq % Hkv) return hipErrorInvalidValue;
   const float2* rt = reinterpret_cast<const float2*>(rope_tab);
   if (ldq % 8 || ldk % 8 || ldv % 8 || ldo % 8 || lddo % 8 || lddq % 8 || lddk % 8 || lddv % 8)
@@ -1332,6 +1333,7 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
     }
 #undef LAUNCH
   }
+  if (mid_event != nullptr) hipEventRecord(mid_event, st);  // between the dQ and dK/dV launches
   if (p2) {
     dim3 g1((S / 128) * Hkv * B);
 #define LAUNCH1(DD, CC)                                                                                       \
@@ -1380,7 +1382,8 @@ hipError_t pra_attn_fwd(int dtype, const void* q, const void* k, const void* v, 
 hipError_t pra_attn_bwd(int dtype, const void* q, const void* k, const void* v, const void* o, const void* dout,
                         const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int S, int Hq, int Hkv,
                         int D, long ldq, long ldk, long ldv, long ldo, long lddo, long lddq, long lddk, long lddv,
-                        float scale, int causal, int skv, const float* rope_tab, hipStream_t st) {
+                        float scale, int causal, int skv, const float* rope_tab, hipEvent_t mid_event,
+                        hipStream_t st) {
   if (skv <= 0 || skv > S) return hipErrorInvalidValue;
   if (dtype == pra::kF32) {
     if (rope_tab != nullptr) return hipErrorInvalidValue;  // the fp32 kernels have no fused inverse RoPE
@@ -1390,10 +1393,10 @@ hipError_t pra_attn_bwd(int dtype, const void* q, const void* k, const void* v, 
   }
   if (dtype == pra::kBF16)
     return attn_bwd_t<__bf16>(q, k, v, o, dout, lse, delta, dq, dk, dv, B, S, Hq, Hkv, D, ldq, ldk, ldv, ldo, lddo,
-                              lddq, lddk, lddv, scale, causal, skv, rope_tab, st);
+                              lddq, lddk, lddv, scale, causal, skv, rope_tab, mid_event, st);
   if (dtype == pra::kF16)
     return attn_bwd_t<_Float16>(q, k, v, o, dout, lse, delta, dq, dk, dv, B, S, Hq, Hkv, D, ldq, ldk, ldv, ldo, lddo,
-                                lddq, lddk, lddv, scale, causal, skv, rope_tab, st);
+                                lddq, lddk, lddv, scale, causal, skv, rope_tab, mid_event, st);
   return hipErrorInvalidValue;
 }
 

@@ -78,7 +78,8 @@ hipError_t pra_attn_fwd(int dtype, const void* q, const void* k, const void* v, 
 hipError_t pra_attn_bwd(int dtype, const void* q, const void* k, const void* v, const void* o, const void* dout,
                         const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int S, int Hq, int Hkv,
                         int D, long ldq, long ldk, long ldv, long ldo, long lddo, long lddq, long lddk, long lddv,
-                        float scale, int causal, int skv, const float* rope_tab, hipStream_t st);
+                        float scale, int causal, int skv, const float* rope_tab, hipEvent_t mid_event,
+                        hipStream_t st);
 void pra_attn_set_options(int fwd_pipe, float fwd_thr, int dkdv_impl, int dq_pipe);
 // fp32 flash attention (attention_f32.hip, f32-input MFMA); pra_attn_fwd / pra_attn_bwd route kF32 here
 hipError_t pra_attn_fwd_f32(const float* q, const float* k, const float* v, float* o, float* lse, int B, int S, int Hq,

@@ -26,6 +26,7 @@ import torch
 
 from .. import _ext
 from . import reference as ref
+from . import sched
 
 
 # ---------------------------------------------------------------------------------------
@@ -424,7 +425,14 @@ def _attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, causal, rope_tab=None) -> 
     if lse is not None and _attn_hip(q, k):
         if q.dtype == torch.float32:
             rope_tab = None  # the fp32 kernels have no fused inverse RoPE: the caller applies it
-        _ext.require_for(q).attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, causal, rope_tab)
+        ev = None
+        if sched.has_hooks():  # a side-stream job waits for the dK/dV kernel (ops/sched.py)
+            ev = torch.cuda.Event()
+            ev.record()  # creates the event; the launcher re-records it between dQ and dK/dV
+        _ext.require_for(q).attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, causal, rope_tab,
+                                     ev.cuda_event if ev is not None else 0)
+        if ev is not None:
+            sched.attention_window(ev)
         return rope_tab is not None
     ct = torch.promote_types(q.dtype, torch.float32)
     with torch.enable_grad():

@@ -16,12 +16,23 @@ from typing import Optional
 import torch
 
 from .. import _ext
+from ..ops import sched
 from ..parallel.flat import FlatParams
 
 # Matrices with a transposed weight shadow (parallel/flat.py) are updated by a tiled AdamW kernel
 # that writes the shadow from the values it just computed (no transpose pass re-reading the
 # weights); PRA_FUSED_ADAMW_T=0 falls back to flat AdamW + a separate transpose.
 FUSED_T = os.environ.get("PRA_FUSED_ADAMW_T", "1") == "1"
+# When an overlapped bucket update is enqueued on the side stream (PYRECOVER_OPT_SCHED):
+#   "attn" (default): held until the next attention backward, then enqueued behind an event recorded
+#            between its dQ and dK/dV kernels (ops.sched.attention_window), so it runs beside dK/dV,
+#            which leaves room on every CU and reads little from HBM;
+#   "eager": as soon as the bucket is reduced (it then lands beside the register-bound dQ kernel and
+#            the memory-bound SwiGLU backward and slows them).
+# Same-process A/B (profiles/r3/step_ab_attnwin_*.log): 7B B16 1063.3 -> 1056.5 ms, 7B B1 99.6 ->
+# 97.9 ms, Llama-3-8B S8192 B1 373.3 -> 361.5 ms, GPT-2-medium unchanged; no update at all: 1043.9
+# ms at B16. (Holding the updates for the W1|W3 / QKV data-gradient GEMMs instead measured +1.45%.)
+OPT_SCHED = os.environ.get("PYRECOVER_OPT_SCHED", "attn")
 
 
 class FlatAdamW(torch.optim.AdamW):
@@ -50,6 +61,7 @@ class FlatAdamW(torch.optim.AdamW):
         self.overlap = False
         self._in_step = False
         self._done_ranges = []
+        self._held = []  # (lo, hi, work) of reduced buckets not yet enqueued (OPT_SCHED "attn")
         self.pre_update_fences = []  # callables run on the update stream before any update
         # graph mode (train.py --compile): step-dependent scalars come from device memory
         self.graph_mode = False
@@ -89,6 +101,7 @@ class FlatAdamW(torch.optim.AdamW):
         self.reducer = reducer
         reducer.hooks.append(self._on_bucket)
         self.stream = torch.cuda.Stream(device=self.flat.data.device) if self.flat.data.is_cuda else None
+        sched.add_attention_window_hook(self.release_held)
 
     def _coeffs(self):
         g = self.param_groups[0]
@@ -140,17 +153,31 @@ class FlatAdamW(torch.optim.AdamW):
             if work is not None:
                 work.wait()
             self._update_range(lo, hi)
-        else:
-            ev = torch.cuda.Event()
-            ev.record()  # compute stream: every read of these weights is already enqueued
-            with torch.cuda.stream(self.stream):
-                self.stream.wait_event(ev)
+            self._done_ranges.append((lo, hi))
+            return
+        self._held.append((lo, hi, work))
+        if OPT_SCHED != "attn":
+            self.release_held()
+
+    def release_held(self, event=None):
+        """Enqueue the held bucket updates on the side stream behind `event` (default: one recorded
+        on the compute stream now). Every read of their weights was enqueued before the bucket was
+        published, so any later point of the compute stream is safe."""
+        if not self._held:
+            return
+        if event is None:
+            event = torch.cuda.Event()
+            event.record()
+        with torch.cuda.stream(self.stream):
+            self.stream.wait_event(event)
+            for lo, hi, work in self._held:
                 if work is not None:
                     work.wait()  # update stream waits for the bucket's all-reduce
                 for fence in self.pre_update_fences:
                     fence()
                 self._update_range(lo, hi)
-        self._done_ranges.append((lo, hi))
+                self._done_ranges.append((lo, hi))
+        self._held = []
 
     def _bind_state(self):
         for p in self.param_groups[0]["params"]:
@@ -180,6 +207,7 @@ class FlatAdamW(torch.optim.AdamW):
             self.reducer.finish()  # launches (and so updates) any bucket not yet ready
             if not self._in_step and not self.graph_mode:  # no bucket fired (no backward this step)
                 self._step += 1
+            self.release_held()
             if self.stream is not None:
                 torch.cuda.current_stream(self.flat.data.device).wait_stream(self.stream)
             self._in_step = False

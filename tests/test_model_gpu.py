@@ -117,6 +117,19 @@ def test_overlapped_optimizer_is_bit_identical(cuda):
     assert torch.equal(p0, p1) and torch.equal(v0, v1)
 
 
+@pytest.mark.parametrize("sched", ["attn", "eager"])
+def test_optimizer_schedules_are_bit_identical(cuda, monkeypatch, sched):
+    """OPT_SCHED "attn" (bucket updates held until the next attention backward and enqueued behind
+    an event between its dQ and dK/dV kernels; the default) and "eager" (enqueued when reduced) only
+    move when the updates run: same parameters and moments as the plain step."""
+    from pyrecover_amd.optim import adamw
+
+    p0, v0, _ = _train_steps(cuda, overlap=False)
+    monkeypatch.setattr(adamw, "OPT_SCHED", sched)
+    p1, v1, _ = _train_steps(cuda, overlap=True)
+    assert torch.equal(p0, p1) and torch.equal(v0, v1)
+
+
 def test_activation_checkpointing_is_bit_identical(cuda):
     """Recomputing each block in backward (with the overlapped per-bucket update running) gives
     the same parameters and moments as keeping the activations."""
