@@ -377,7 +377,7 @@ void xent_bwd_(at::Tensor logits, const at::Tensor& labels, const at::Tensor& ls
 
 void adamw_flat_(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, double lr, double b1, double b2,
                  double eps, double wd, double bc1, double bc2_sqrt, double gscale,
-                 const c10::optional<at::Tensor>& gscale_dev, const c10::optional<at::Tensor>& hyper_dev) {
+                 const c10::optional<at::Tensor>& gscale_dev, const c10::optional<at::Tensor>& hyper_dev, bool fast) {
   const Range range_("pyrecover::adamw_flat");
   check_dev(p, "p");
   TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous(), "adamw: contiguous");
@@ -401,14 +401,14 @@ void adamw_flat_(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, 
   }
   check(pra_adamw_flat(dt(p), dt(m), p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), (float)lr,
                        (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1, (float)bc2_sqrt, (float)gscale, gsd,
-                       hyd, stream_of(p)),
+                       hyd, fast ? 1 : 0, stream_of(p)),
         "adamw_flat");
 }
 
 // AdamW of one row-major weight matrix p [rows, cols] that also writes pt = p^T [cols, rows].
 void adamw_t_(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, at::Tensor pt, double lr, double b1,
               double b2, double eps, double wd, double bc1, double bc2_sqrt, double gscale,
-              const c10::optional<at::Tensor>& gscale_dev, const c10::optional<at::Tensor>& hyper_dev) {
+              const c10::optional<at::Tensor>& gscale_dev, const c10::optional<at::Tensor>& hyper_dev, bool fast) {
   const Range range_("pyrecover::adamw_t");
   check_dev(p, "p");
   TORCH_CHECK(p.dim() == 2 && p.is_contiguous() && g.sizes() == p.sizes() && m.sizes() == p.sizes() &&
@@ -439,7 +439,7 @@ void adamw_t_(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, at:
   }
   check(pra_adamw_t(dt(p), p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), pt.data_ptr(), (int)rows,
                     (int)cols, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1, (float)bc2_sqrt,
-                    (float)gscale, gsd, hyd, stream_of(p)),
+                    (float)gscale, gsd, hyd, fast ? 1 : 0, stream_of(p)),
         "adamw_t");
 }
 
@@ -764,10 +764,12 @@ PYBIND11_MODULE(_C, m) {
   namespace py = pybind11;
   m.def("adamw_flat_", &adamw_flat_, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("lr"),
         py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("bc1"), py::arg("bc2_sqrt"),
-        py::arg("gscale"), py::arg("gscale_dev") = py::none(), py::arg("hyper_dev") = py::none());
+        py::arg("gscale"), py::arg("gscale_dev") = py::none(), py::arg("hyper_dev") = py::none(),
+        py::arg("fast") = false);
   m.def("adamw_t_", &adamw_t_, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("pt"), py::arg("lr"),
         py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("bc1"), py::arg("bc2_sqrt"),
-        py::arg("gscale"), py::arg("gscale_dev") = py::none(), py::arg("hyper_dev") = py::none());
+        py::arg("gscale"), py::arg("gscale_dev") = py::none(), py::arg("hyper_dev") = py::none(),
+        py::arg("fast") = false);
   m.def("grad_norm", &grad_norm);
   m.def("wgrad_mm_", &wgrad_mm_);
   m.def("wgrad_mm_exp_", &wgrad_mm_exp_);

@@ -20,17 +20,28 @@ namespace pra {
 
 // One AdamW element update with every fused multiply-add written out, so all kernels that use it
 // (flat, tiled + transposed) round identically whatever the compiler's contraction choices.
+// FAST: the two divisions and the square root on the hardware v_rcp_f32 / v_sqrt_f32 (1 ulp each)
+// instead of the correctly rounded IEEE sequences (~10 VALU per division): ~17 instead of ~60 VALU
+// per element, which matters because the update runs beside the attention backward on a side
+// stream. m and v are computed exactly as before; p's update term differs by at most a few fp32
+// ulps before its bf16 rounding. !FAST keeps torch _fused_adamw_'s correctly rounded divisions.
+template <bool FAST>
 __device__ __forceinline__ void adamw_elem(float& p, float& m, float& v, float g, float gs, float decay, float b1,
                                            float b2, float eps, float bc2_sqrt, float step_size) {
   const float gr = g * gs;
   p *= decay;
   m = fmaf(1.f - b1, gr - m, m);
   v = fmaf(b2, v, (1.f - b2) * (gr * gr));
-  const float denom = __fdiv_rn(sqrtf(v), bc2_sqrt) + eps;
-  p = fmaf(-step_size, __fdiv_rn(m, denom), p);
+  if constexpr (FAST) {
+    const float denom = fmaf(__builtin_amdgcn_sqrtf(v), __builtin_amdgcn_rcpf(bc2_sqrt), eps);
+    p = fmaf(-step_size, m * __builtin_amdgcn_rcpf(denom), p);
+  } else {
+    const float denom = __fdiv_rn(sqrtf(v), bc2_sqrt) + eps;
+    p = fmaf(-step_size, __fdiv_rn(m, denom), p);
+  }
 }
 
-template <typename P, typename S>
+template <typename P, typename S, bool FAST>
 __global__ __launch_bounds__(256) void adamw_kernel(P* __restrict__ p, const P* __restrict__ g, S* __restrict__ m,
                                                     S* __restrict__ v, long n, float lr, float b1, float b2,
                                                     float eps, float wd, float bc1, float bc2_sqrt, float gscale,
@@ -53,7 +64,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(P* __restrict__ p, const P* 
     load8<S>(m + o, mv);
     load8<S>(v + o, vv);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) adamw_elem(pv[j], mv[j], vv[j], gv[j], gs, decay, b1, b2, eps, bc2_sqrt, step_size);
+    for (int j = 0; j < 8; ++j) adamw_elem<FAST>(pv[j], mv[j], vv[j], gv[j], gs, decay, b1, b2, eps, bc2_sqrt, step_size);
     store8<P>(p + o, pv);
     store8<S>(m + o, mv);
     store8<S>(v + o, vv);
@@ -61,7 +72,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(P* __restrict__ p, const P* 
   // tail
   for (long o = n8 * 8 + (long)blockIdx.x * 256 + threadIdx.x; o < n; o += (long)gridDim.x * 256) {
     float pv = to_f<P>(p[o]), mv = to_f<S>(m[o]), vv = to_f<S>(v[o]);
-    adamw_elem(pv, mv, vv, to_f<P>(g[o]), gs, decay, b1, b2, eps, bc2_sqrt, step_size);
+    adamw_elem<FAST>(pv, mv, vv, to_f<P>(g[o]), gs, decay, b1, b2, eps, bc2_sqrt, step_size);
     p[o] = from_f<P>(pv);
     m[o] = from_f<S>(mv);
     v[o] = from_f<S>(vv);
@@ -73,7 +84,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(P* __restrict__ p, const P* 
 // updated values it already holds: the separate transpose pass re-read the whole model after
 // every update (13.5 GB/step at 7B). Block = one 64 x 64 tile; the updated p tile goes through
 // LDS (padded rows) to 16-B transposed stores. Same math and rounding as adamw_kernel.
-template <typename P>
+template <typename P, bool FAST>
 __global__ __launch_bounds__(256) void adamw_t_kernel(P* __restrict__ p, const P* __restrict__ g, P* __restrict__ m,
                                                       P* __restrict__ v, P* __restrict__ pt, int rows, int cols,
                                                       float lr, float b1, float b2, float eps, float wd, float bc1,
@@ -99,7 +110,7 @@ __global__ __launch_bounds__(256) void adamw_t_kernel(P* __restrict__ p, const P
     load8<P>(m + o, mv);
     load8<P>(v + o, vv);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) adamw_elem(pv[j], mv[j], vv[j], gv[j], gs, decay, b1, b2, eps, bc2_sqrt, step_size);
+    for (int j = 0; j < 8; ++j) adamw_elem<FAST>(pv[j], mv[j], vv[j], gv[j], gs, decay, b1, b2, eps, bc2_sqrt, step_size);
     store8<P>(p + o, pv);
     store8<P>(m + o, mv);
     store8<P>(v + o, vv);
@@ -159,15 +170,22 @@ extern "C" {
 // pdtype: param/grad dtype; sdtype: moment dtype
 hipError_t pra_adamw_flat(int pdtype, int sdtype, void* p, const void* g, void* m, void* v, long n, float lr,
                           float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt, float gscale,
-                          const float* gscale_dev, const float* hyper_dev, hipStream_t s) {
+                          const float* gscale_dev, const float* hyper_dev, int fast, hipStream_t s) {
   long blocks = (n / 8 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
   if (pdtype != sdtype) return hipErrorInvalidValue;
-  PRA_DISPATCH_FLOAT(pdtype, T,
-                     hipLaunchKernelGGL((pra::adamw_kernel<T, T>), dim3(blocks), dim3(256), 0, s, (T*)p, (const T*)g,
-                                        (T*)m, (T*)v, n, lr, b1, b2, eps, wd, bc1, bc2_sqrt, gscale, gscale_dev,
-                                        hyper_dev));
+  if (fast) {
+    PRA_DISPATCH_FLOAT(pdtype, T,
+                       hipLaunchKernelGGL((pra::adamw_kernel<T, T, true>), dim3(blocks), dim3(256), 0, s, (T*)p,
+                                          (const T*)g, (T*)m, (T*)v, n, lr, b1, b2, eps, wd, bc1, bc2_sqrt, gscale,
+                                          gscale_dev, hyper_dev));
+  } else {
+    PRA_DISPATCH_FLOAT(pdtype, T,
+                       hipLaunchKernelGGL((pra::adamw_kernel<T, T, false>), dim3(blocks), dim3(256), 0, s, (T*)p,
+                                          (const T*)g, (T*)m, (T*)v, n, lr, b1, b2, eps, wd, bc1, bc2_sqrt, gscale,
+                                          gscale_dev, hyper_dev));
+  }
   return hipGetLastError();
 }
 
@@ -175,16 +193,23 @@ hipError_t pra_adamw_flat(int pdtype, int sdtype, void* p, const void* g, void* 
 // 16-bit params, moments of the same dtype).
 hipError_t pra_adamw_t(int dtype, void* p, const void* g, void* m, void* v, void* pt, int rows, int cols, float lr,
                        float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt, float gscale,
-                       const float* gscale_dev, const float* hyper_dev, hipStream_t s) {
+                       const float* gscale_dev, const float* hyper_dev, int fast, hipStream_t s) {
   if (rows % 64 || cols % 64 || rows <= 0 || cols <= 0) return hipErrorInvalidValue;
   // (A strip kernel walking 4 tiles per block was faster in isolation, 22.7 -> 21.3 ms per 7B step,
   // but slower overlapped with the backward GEMMs on the side stream: 1074.5 vs 1069.6 ms/step,
   // profiles/adamw_t_strip_ab_r2.log. Removed.)
   const dim3 grid(cols / 64, rows / 64);
-  PRA_DISPATCH_16BIT(dtype, T,
-                     hipLaunchKernelGGL((pra::adamw_t_kernel<T>), grid, dim3(256), 0, s, (T*)p, (const T*)g, (T*)m,
-                                        (T*)v, (T*)pt, rows, cols, lr, b1, b2, eps, wd, bc1, bc2_sqrt, gscale,
-                                        gscale_dev, hyper_dev));
+  if (fast) {
+    PRA_DISPATCH_16BIT(dtype, T,
+                       hipLaunchKernelGGL((pra::adamw_t_kernel<T, true>), grid, dim3(256), 0, s, (T*)p, (const T*)g,
+                                          (T*)m, (T*)v, (T*)pt, rows, cols, lr, b1, b2, eps, wd, bc1, bc2_sqrt,
+                                          gscale, gscale_dev, hyper_dev));
+  } else {
+    PRA_DISPATCH_16BIT(dtype, T,
+                       hipLaunchKernelGGL((pra::adamw_t_kernel<T, false>), grid, dim3(256), 0, s, (T*)p, (const T*)g,
+                                          (T*)m, (T*)v, (T*)pt, rows, cols, lr, b1, b2, eps, wd, bc1, bc2_sqrt,
+                                          gscale, gscale_dev, hyper_dev));
+  }
   return hipGetLastError();
 }
 

@@ -33,6 +33,9 @@ FUSED_T = os.environ.get("PRA_FUSED_ADAMW_T", "1") == "1"
 # 97.9 ms, Llama-3-8B S8192 B1 373.3 -> 361.5 ms, GPT-2-medium unchanged; no update at all: 1043.9
 # ms at B16. (Holding the updates for the W1|W3 / QKV data-gradient GEMMs instead measured +1.45%.)
 OPT_SCHED = os.environ.get("PYRECOVER_OPT_SCHED", "attn")
+# PYRECOVER_ADAMW_FAST=1: hardware reciprocal / square root in the update (csrc/kernels/optim.hip
+# adamw_elem<FAST>); 0: torch _fused_adamw_'s correctly rounded divisions
+FAST_MATH = os.environ.get("PYRECOVER_ADAMW_FAST", "0") == "1"
 
 
 class FlatAdamW(torch.optim.AdamW):
@@ -119,9 +122,11 @@ class FlatAdamW(torch.optim.AdamW):
         args = (lr, b1, b2, eps, wd, bc1, bc2_sqrt, self.grad_scale, self.grad_scale_dev, self.hyper)
         m, v = self.exp_avg, self.exp_avg_sq
 
+        fast = FAST_MATH
+
         def flat_update(a, b):
             if a < b:
-                C.adamw_flat_(f.data[a:b], f.grad[a:b], m[a:b], v[a:b], *args)
+                C.adamw_flat_(f.data[a:b], f.grad[a:b], m[a:b], v[a:b], *args, fast)
 
         mats = f.transposed_in(lo, hi) if FUSED_T else []
         cur = lo
@@ -134,7 +139,7 @@ class FlatAdamW(torch.optim.AdamW):
             flat_update(cur, o)
             sl = slice(o, o + n)
             C.adamw_t_(f.data[sl].view(rows, cols), f.grad[sl].view(rows, cols), m[sl].view(rows, cols),
-                       v[sl].view(rows, cols), f.data_t[sl].view(cols, rows), *args)
+                       v[sl].view(rows, cols), f.data_t[sl].view(cols, rows), *args, fast)
             cur = o + n
         flat_update(cur, hi)
         if not FUSED_T:

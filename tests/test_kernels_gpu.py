@@ -146,7 +146,10 @@ def test_cross_entropy(cuda, V):
     assert d[:13].abs().max().item() == 0
 
 
-def test_adamw_matches_torch_fused(cuda):
+@pytest.mark.parametrize("fast", [False, True])
+def test_adamw_matches_torch_fused(cuda, fast):
+    """Correctly rounded divisions (fast=False) and the hardware reciprocal / square root
+    (fast=True) both track torch's fused AdamW."""
     C = _ext.native()
     n = 1 << 20
     torch.manual_seed(1)
@@ -158,7 +161,7 @@ def test_adamw_matches_torch_fused(cuda):
     step = torch.zeros((), device=cuda)
     lr, b1, b2, eps, wd = 1e-3, 0.9, 0.999, 1e-8, 0.01
     for s in range(1, 4):
-        C.adamw_flat_(p, g, m, v, lr, b1, b2, eps, wd, 1 - b1 ** s, math.sqrt(1 - b2 ** s), 1.0, None)
+        C.adamw_flat_(p, g, m, v, lr, b1, b2, eps, wd, 1 - b1 ** s, math.sqrt(1 - b2 ** s), 1.0, None, None, fast)
         step += 1
         torch._fused_adamw_([p2], [g], [m2], [v2], [], [step], amsgrad=False, lr=lr, beta1=b1, beta2=b2,
                             weight_decay=wd, eps=eps, maximize=False)
@@ -400,7 +403,8 @@ def test_rope_t_matches_rope_exactly(cuda):
 
 @pytest.mark.parametrize("rows,cols", [(64, 64), (192, 320), (4096, 128), (128, 512)])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-def test_adamw_t_matches_flat_adamw_plus_transpose(cuda, rows, cols, dtype):
+@pytest.mark.parametrize("fast", [False, True])
+def test_adamw_t_matches_flat_adamw_plus_transpose(cuda, rows, cols, dtype, fast):
     """Fused AdamW + transposed-shadow write == flat AdamW followed by transpose2d, bit for bit
     (incl. device-side grad scale and hyper-parameters)."""
     C = _ext.native()
@@ -413,11 +417,11 @@ def test_adamw_t_matches_flat_adamw_plus_transpose(cuda, rows, cols, dtype):
     hy = torch.tensor([3e-4, 0.19, 0.031], device=cuda)
     a = [t.clone() for t in (p, g, m, v)]
     C.adamw_flat_(a[0].view(-1), a[1].view(-1), a[2].view(-1), a[3].view(-1), 1e-3, 0.9, 0.95, 1e-8, 0.1, 0.5, 0.2,
-                  0.5, gs, hy)
+                  0.5, gs, hy, fast)
     pt_ref = C.transpose2d(a[0])
     b = [t.clone() for t in (p, g, m, v)]
     pt = torch.empty(cols, rows, device=cuda, dtype=dtype)
-    C.adamw_t_(b[0], b[1], b[2], b[3], pt, 1e-3, 0.9, 0.95, 1e-8, 0.1, 0.5, 0.2, 0.5, gs, hy)
+    C.adamw_t_(b[0], b[1], b[2], b[3], pt, 1e-3, 0.9, 0.95, 1e-8, 0.1, 0.5, 0.2, 0.5, gs, hy, fast)
     for x, y in zip(a, b):
         assert torch.equal(x, y)
     assert torch.equal(pt, pt_ref)
