@@ -4,7 +4,9 @@
 // flat, identically-ordered device buffers, so the optimizer step is ONE streaming kernel
 // over N elements (14 B/elem for bf16 p/g/m/v: read 8, write 6) instead of a multi-tensor
 // launch list. Math follows torch's fused AdamW (`_fused_adamw_`, used by the reference's
-// `--fused-optimizer`, train.py:120-122): fp32 opmath, one rounding per stored value.
+// `--fused-optimizer`, train.py:120-122): fp32 opmath, one rounding per stored value; the default
+// FAST instantiation takes the two divisions and the square root from the hardware (1 ulp) instead
+// of torch's correctly rounded sequences (see adamw_elem).
 //
 //   p  = p * (1 - lr*wd)
 //   m  = lerp(m, g, 1-b1)            v = b2*v + (1-b2)*g*g

@@ -33,9 +33,11 @@ FUSED_T = os.environ.get("PRA_FUSED_ADAMW_T", "1") == "1"
 # 97.9 ms, Llama-3-8B S8192 B1 373.3 -> 361.5 ms, GPT-2-medium unchanged; no update at all: 1043.9
 # ms at B16. (Holding the updates for the W1|W3 / QKV data-gradient GEMMs instead measured +1.45%.)
 OPT_SCHED = os.environ.get("PYRECOVER_OPT_SCHED", "attn")
-# PYRECOVER_ADAMW_FAST=1: hardware reciprocal / square root in the update (csrc/kernels/optim.hip
-# adamw_elem<FAST>); 0: torch _fused_adamw_'s correctly rounded divisions
-FAST_MATH = os.environ.get("PYRECOVER_ADAMW_FAST", "0") == "1"
+# PYRECOVER_ADAMW_FAST (default 1): hardware reciprocal / square root in the update
+# (csrc/kernels/optim.hip adamw_elem<FAST>: ~17 instead of ~60 VALU per element, which matters
+# beside the attention backward; 7B B1 98.5 -> 97.2 ms, B16 -0.15%, profiles/r3/step_ab_fast_*.log);
+# 0: torch _fused_adamw_'s correctly rounded divisions (p's update term differs by a few fp32 ulps)
+FAST_MATH = os.environ.get("PYRECOVER_ADAMW_FAST", "1") == "1"
 
 
 class FlatAdamW(torch.optim.AdamW):
