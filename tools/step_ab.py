@@ -25,8 +25,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def parse_arm(spec):
-    """`opt.ATTR=value` sets an attribute of the optimizer instance; the item `noupdate` skips the
-    AdamW update kernels (a diagnostic arm: what the optimizer costs the step)."""
+    """`opt.ATTR=value` sets an attribute of the optimizer instance; `attn.OPTION=value` an
+    attention kernel option (_ext.set_attn_options); the item `noupdate` skips the AdamW update
+    kernels (a diagnostic arm: what the optimizer costs the step)."""
     name, _, body = spec.partition(":")
     sets = []
     for item in filter(None, body.split(";")):
@@ -35,6 +36,9 @@ def parse_arm(spec):
             continue
         lhs, _, rhs = item.partition("=")
         mod, _, attr = lhs.strip().rpartition(".")
+        if mod == "attn":
+            sets.append(("attn", attr, ast.literal_eval(rhs.strip())))
+            continue
         target = "opt" if mod == "opt" else importlib.import_module("pyrecover_amd." + mod)
         sets.append((target, attr, ast.literal_eval(rhs.strip())))
     return name, sets
@@ -85,9 +89,13 @@ def main():
         opt.step()
         return loss
 
+    from pyrecover_amd import _ext
+
     def resolve(sets):
         out = []
         for m, k, v in sets:
+            if m == "attn":
+                continue
             m = opt if m == "opt" else m
             if v == "noupdate":
                 v = lambda *args, **kw: None  # noqa: E731
@@ -95,6 +103,8 @@ def main():
         return out
 
     def run(arm, n):
+        attn = {k: v for m, k, v in arm[1] if m == "attn"}
+        prev_attn = _ext.set_attn_options(**attn) if attn else None
         sets = resolve(arm[1])
         old = [(m, k, m.__dict__[k] if k in m.__dict__ else getattr(m, k)) for m, k, _ in sets]
         for m, k, v in sets:
@@ -107,6 +117,8 @@ def main():
             torch.cuda.synchronize()
             return (time.perf_counter() - t0) * 1000 / n, float(loss.item())
         finally:
+            if prev_attn is not None:
+                _ext.set_attn_options(**prev_attn)
             for m, k, v in old:
                 if m is opt and k == "_update_range":
                     del m.__dict__[k]  # back to the class method
