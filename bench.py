@@ -73,6 +73,13 @@ def launch_command(argv, gpus: int, env) -> list:
             "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + list(argv)
 
 
+def _opt_sched() -> str:
+    from pyrecover_amd.optim import adamw
+
+    return {"attn": "beside the attention dK/dV kernels", "eager": "per bucket as reduced"}.get(
+        adamw.OPT_SCHED, adamw.OPT_SCHED)
+
+
 def main():
     args = parse()
     cmd = launch_command(sys.argv[1:], args.gpus, os.environ)
@@ -242,7 +249,8 @@ def main():
                        "dist_backend": torch.distributed.get_backend() if world > 1 else None,
                        "grad_buckets": reducer.num_buckets,
                        "rccl_high_priority_stream": os.environ.get("PYRECOVER_RCCL_HIGH_PRIORITY", "1") == "1",
-                       "optimizer": "AdamW (flat fused HIP)" + ("" if args.no_overlap_optimizer else ", overlapped with backward")},
+                       "optimizer": "AdamW (flat fused HIP)" + ("" if args.no_overlap_optimizer else
+                                                                 f", overlapped with backward ({_opt_sched()})")},
             "tokens_per_sec_per_gpu": round(tps / world, 2),
             "model_tflops_per_gpu": round(fpt * tps / world / 1e12, 2),
             "mfu_pct_vs_2.5PF": round(100 * fpt * tps / world / 2.5e15, 2),
