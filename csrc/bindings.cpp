@@ -393,14 +393,14 @@ void adamw_flat_(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, 
     same_dev(p, *gscale_dev, "gscale_dev");
     gsd = gscale_dev->data_ptr<float>();
   }
-  const float* hyd = nullptr;
+  const double* hyd = nullptr;
   if (hyper_dev.has_value()) {
-    TORCH_CHECK(hyper_dev->scalar_type() == at::kFloat && hyper_dev->numel() >= 3, "adamw: hyper_dev fp32[3]");
+    TORCH_CHECK(hyper_dev->scalar_type() == at::kDouble && hyper_dev->numel() >= 3, "adamw: hyper_dev fp64[3]");
     same_dev(p, *hyper_dev, "hyper_dev");
-    hyd = hyper_dev->data_ptr<float>();
+    hyd = hyper_dev->data_ptr<double>();
   }
-  check(pra_adamw_flat(dt(p), dt(m), p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), (float)lr,
-                       (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1, (float)bc2_sqrt, (float)gscale, gsd,
+  check(pra_adamw_flat(dt(p), dt(m), p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), lr, b1,
+                       b2, eps, wd, bc1, bc2_sqrt, (float)gscale, gsd,
                        hyd, fast ? 1 : 0, stream_of(p)),
         "adamw_flat");
 }
@@ -431,15 +431,14 @@ void adamw_t_(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, at:
     same_dev(p, *gscale_dev, "gscale_dev");
     gsd = gscale_dev->data_ptr<float>();
   }
-  const float* hyd = nullptr;
+  const double* hyd = nullptr;
   if (hyper_dev.has_value()) {
-    TORCH_CHECK(hyper_dev->scalar_type() == at::kFloat && hyper_dev->numel() >= 3, "adamw_t: hyper_dev fp32[3]");
+    TORCH_CHECK(hyper_dev->scalar_type() == at::kDouble && hyper_dev->numel() >= 3, "adamw_t: hyper_dev fp64[3]");
     same_dev(p, *hyper_dev, "hyper_dev");
-    hyd = hyper_dev->data_ptr<float>();
+    hyd = hyper_dev->data_ptr<double>();
   }
   check(pra_adamw_t(dt(p), p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), pt.data_ptr(), (int)rows,
-                    (int)cols, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1, (float)bc2_sqrt,
-                    (float)gscale, gsd, hyd, fast ? 1 : 0, stream_of(p)),
+                    (int)cols, lr, b1, b2, eps, wd, bc1, bc2_sqrt, (float)gscale, gsd, hyd, fast ? 1 : 0, stream_of(p)),
         "adamw_t");
 }
 

@@ -58,18 +58,18 @@ hipError_t pra_xent_fwd(int dtype, const void* logits, const int64_t* labels, fl
 hipError_t pra_xent_bwd(int dtype, void* logits, const int64_t* labels, const float* lse, const float* stats,
                         const float* grad_out, long T, long V, long ld, long ignore_index, hipStream_t s);
 
-hipError_t pra_adamw_flat(int pdtype, int sdtype, void* p, const void* g, void* m, void* v, long n, float lr,
-                          float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt, float gscale,
-                          const float* gscale_dev, const float* hyper_dev, int fast, hipStream_t s);
+hipError_t pra_adamw_flat(int pdtype, int sdtype, void* p, const void* g, void* m, void* v, long n, double lr,
+                          double b1, double b2, double eps, double wd, double bc1, double bc2_sqrt, float gscale,
+                          const float* gscale_dev, const double* hyper_dev, int fast, hipStream_t s);
 int pra_sumsq_partials();
 hipError_t pra_grad_norm(int dtype, const void* x, long n, float* ws, float* out, float max_norm, float pre_scale,
                          hipStream_t s);
 
 hipError_t pra_sum_slices(int dtype, const void* const* srcs, int nsrc, void* dst, long n, hipStream_t s);
 
-hipError_t pra_adamw_t(int dtype, void* p, const void* g, void* m, void* v, void* pt, int rows, int cols, float lr,
-                       float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt, float gscale,
-                       const float* gscale_dev, const float* hyper_dev, int fast, hipStream_t s);
+hipError_t pra_adamw_t(int dtype, void* p, const void* g, void* m, void* v, void* pt, int rows, int cols, double lr,
+                       double b1, double b2, double eps, double wd, double bc1, double bc2_sqrt, float gscale,
+                       const float* gscale_dev, const double* hyper_dev, int fast, hipStream_t s);
 
 hipError_t pra_attn_fwd(int dtype, const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int Hq,
                         int Hkv, int D, long ldq, long ldk, long ldv, long ldo, float scale, int causal,

@@ -4,12 +4,14 @@
 // flat, identically-ordered device buffers, so the optimizer step is ONE streaming kernel
 // over N elements (14 B/elem for bf16 p/g/m/v: read 8, write 6) instead of a multi-tensor
 // launch list. Math follows torch's fused AdamW (`_fused_adamw_`, used by the reference's
-// `--fused-optimizer`, train.py:120-122): fp32 opmath, one rounding per stored value; the default
-// FAST instantiation takes the two divisions and the square root from the hardware (1 ulp) instead
-// of torch's correctly rounded sequences (see adamw_elem).
+// `--fused-optimizer`, train.py:120-122) bit for bit in the default (!FAST) instantiation: the same
+// mixed fp64/fp32 expression tree as ATen's adam_math (ATen/native/hip/fused_adam_utils.cuh: double
+// lr/betas/eps/weight decay against fp32 values, fp32 bias corrections, correctly rounded fp32
+// division and square root). The FAST instantiation (opt-in) takes the two divisions and the square
+// root from the hardware (1 ulp) in pure fp32 (see adamw_elem).
 //
-//   p  = p * (1 - lr*wd)
-//   m  = lerp(m, g, 1-b1)            v = b2*v + (1-b2)*g*g
+//   p  = p - lr*wd*p
+//   m  = b1*m + (1-b1)*g             v = b2*v + (1-b2)*g*g
 //   p  = p - (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)
 //
 // `gscale` pre-multiplies the gradient (1/world_size after a SUM all-reduce, and/or a
@@ -20,43 +22,71 @@
 
 namespace pra {
 
-// One AdamW element update with every fused multiply-add written out, so all kernels that use it
-// (flat, tiled + transposed) round identically whatever the compiler's contraction choices.
-// FAST: the two divisions and the square root on the hardware v_rcp_f32 / v_sqrt_f32 (1 ulp each)
-// instead of the correctly rounded IEEE sequences (~10 VALU per division): ~17 instead of ~60 VALU
-// per element, which matters because the update runs beside the attention backward on a side
-// stream. m and v are computed exactly as before; p's update term differs by at most a few fp32
-// ulps before its bf16 rounding. !FAST keeps torch _fused_adamw_'s correctly rounded divisions.
-template <bool FAST>
-__device__ __forceinline__ void adamw_elem(float& p, float& m, float& v, float g, float gs, float decay, float b1,
-                                           float b2, float eps, float bc2_sqrt, float step_size) {
-  const float gr = g * gs;
-  p *= decay;
-  m = fmaf(1.f - b1, gr - m, m);
-  v = fmaf(b2, v, (1.f - b2) * (gr * gr));
-  if constexpr (FAST) {
-    const float denom = fmaf(__builtin_amdgcn_sqrtf(v), __builtin_amdgcn_rcpf(bc2_sqrt), eps);
-    p = fmaf(-step_size, m * __builtin_amdgcn_rcpf(denom), p);
-  } else {
-    const float denom = __fdiv_rn(sqrtf(v), bc2_sqrt) + eps;
-    p = fmaf(-step_size, __fdiv_rn(m, denom), p);
-  }
-}
+// Scalars of one update, prepared once per thread from the host (or device, graph mode) values.
+struct AdamCoef {
+  double lr_wd, b1, b2, eps;  // torch's double hyper-parameters
+  float bc2f, step_size;      // torch's fp32 bias correction and (float)(lr / bc1_f)
+  float decay, b1f, b2f, epsf, rbc2;  // FAST: pure fp32 forms
+};
 
-template <typename P, typename S, bool FAST>
-__global__ __launch_bounds__(256) void adamw_kernel(P* __restrict__ p, const P* __restrict__ g, S* __restrict__ m,
-                                                    S* __restrict__ v, long n, float lr, float b1, float b2,
-                                                    float eps, float wd, float bc1, float bc2_sqrt, float gscale,
-                                                    const float* __restrict__ gscale_dev,
-                                                    const float* __restrict__ hyper_dev) {
-  const float gs = gscale_dev ? gscale * gscale_dev[0] : gscale;
+__device__ __forceinline__ AdamCoef adam_coef(double lr, double b1, double b2, double eps, double wd, double bc1,
+                                              double bc2_sqrt, const double* __restrict__ hyper_dev) {
   if (hyper_dev) {  // step-dependent scalars from device memory (graph-captured step)
     lr = hyper_dev[0];
     bc1 = hyper_dev[1];
     bc2_sqrt = hyper_dev[2];
   }
-  const float decay = 1.f - lr * wd;
-  const float step_size = lr / bc1;
+  AdamCoef c;
+  c.lr_wd = lr * wd;
+  c.b1 = b1;
+  c.b2 = b2;
+  c.eps = eps;
+  const float bc1f = (float)bc1;  // ATen passes the double bias corrections as opmath_t (fp32)
+  c.bc2f = (float)bc2_sqrt;
+  c.step_size = (float)(lr / (double)bc1f);
+  c.decay = (float)(1.0 - c.lr_wd);
+  c.b1f = (float)b1;
+  c.b2f = (float)b2;
+  c.epsf = (float)eps;
+  c.rbc2 = __builtin_amdgcn_rcpf(c.bc2f);
+  return c;
+}
+
+// One AdamW element update with every fused multiply-add written out, so all kernels that use it
+// (flat, tiled + transposed) round identically whatever the compiler's contraction choices.
+// !FAST: ATen adam_math's expression tree. Its double sub-expressions are contracted the way hipcc
+// contracts ATen's source (fadd(fmul a b, fmul c d) -> fma(a, b, c*d); p - x*p -> fma(-x, p, p));
+// each is rounded once to fp32, then the fp32 tail (step_size*m)/denom is correctly rounded.
+// FAST: the two divisions and the square root on the hardware v_rcp_f32 / v_sqrt_f32 (1 ulp each),
+// all in fp32: ~17 instead of ~60 VALU per element. p differs from torch by a few fp32 ulps before
+// its bf16 rounding (opt-in: PYRECOVER_ADAMW_FAST=1).
+template <bool FAST>
+__device__ __forceinline__ void adamw_elem(float& p, float& m, float& v, float g, float gs, const AdamCoef& c) {
+  const float gr = g * gs;
+  if constexpr (FAST) {
+    p *= c.decay;
+    m = fmaf(1.f - c.b1f, gr - m, m);
+    v = fmaf(c.b2f, v, (1.f - c.b2f) * (gr * gr));
+    const float denom = fmaf(__builtin_amdgcn_sqrtf(v), c.rbc2, c.epsf);
+    p = fmaf(-c.step_size, m * __builtin_amdgcn_rcpf(denom), p);
+  } else {
+    const double pd = (double)p, gd = (double)gr;
+    p = (float)fma(-c.lr_wd, pd, pd);
+    m = (float)fma(c.b1, (double)m, (1.0 - c.b1) * gd);
+    v = (float)fma(c.b2, (double)v, ((1.0 - c.b2) * gd) * gd);
+    const float denom = (float)((double)__fdiv_rn(__fsqrt_rn(v), c.bc2f) + c.eps);
+    p = p - __fdiv_rn(c.step_size * m, denom);
+  }
+}
+
+template <typename P, typename S, bool FAST>
+__global__ __launch_bounds__(256) void adamw_kernel(P* __restrict__ p, const P* __restrict__ g, S* __restrict__ m,
+                                                    S* __restrict__ v, long n, double lr, double b1, double b2,
+                                                    double eps, double wd, double bc1, double bc2_sqrt, float gscale,
+                                                    const float* __restrict__ gscale_dev,
+                                                    const double* __restrict__ hyper_dev) {
+  const float gs = gscale_dev ? gscale * gscale_dev[0] : gscale;
+  const AdamCoef c = adam_coef(lr, b1, b2, eps, wd, bc1, bc2_sqrt, hyper_dev);
   const long n8 = n / 8;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
     const long o = i * 8;
@@ -66,7 +96,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(P* __restrict__ p, const P* 
     load8<S>(m + o, mv);
     load8<S>(v + o, vv);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) adamw_elem<FAST>(pv[j], mv[j], vv[j], gv[j], gs, decay, b1, b2, eps, bc2_sqrt, step_size);
+    for (int j = 0; j < 8; ++j) adamw_elem<FAST>(pv[j], mv[j], vv[j], gv[j], gs, c);
     store8<P>(p + o, pv);
     store8<S>(m + o, mv);
     store8<S>(v + o, vv);
@@ -74,7 +104,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(P* __restrict__ p, const P* 
   // tail
   for (long o = n8 * 8 + (long)blockIdx.x * 256 + threadIdx.x; o < n; o += (long)gridDim.x * 256) {
     float pv = to_f<P>(p[o]), mv = to_f<S>(m[o]), vv = to_f<S>(v[o]);
-    adamw_elem<FAST>(pv, mv, vv, to_f<P>(g[o]), gs, decay, b1, b2, eps, bc2_sqrt, step_size);
+    adamw_elem<FAST>(pv, mv, vv, to_f<P>(g[o]), gs, c);
     p[o] = from_f<P>(pv);
     m[o] = from_f<S>(mv);
     v[o] = from_f<S>(vv);
@@ -89,18 +119,13 @@ __global__ __launch_bounds__(256) void adamw_kernel(P* __restrict__ p, const P* 
 template <typename P, bool FAST>
 __global__ __launch_bounds__(256) void adamw_t_kernel(P* __restrict__ p, const P* __restrict__ g, P* __restrict__ m,
                                                       P* __restrict__ v, P* __restrict__ pt, int rows, int cols,
-                                                      float lr, float b1, float b2, float eps, float wd, float bc1,
-                                                      float bc2_sqrt, float gscale, const float* __restrict__ gscale_dev,
-                                                      const float* __restrict__ hyper_dev) {
+                                                      double lr, double b1, double b2, double eps, double wd,
+                                                      double bc1, double bc2_sqrt, float gscale,
+                                                      const float* __restrict__ gscale_dev,
+                                                      const double* __restrict__ hyper_dev) {
   __shared__ uint16_t tile[64][72];
   const float gs = gscale_dev ? gscale * gscale_dev[0] : gscale;
-  if (hyper_dev) {
-    lr = hyper_dev[0];
-    bc1 = hyper_dev[1];
-    bc2_sqrt = hyper_dev[2];
-  }
-  const float decay = 1.f - lr * wd;
-  const float step_size = lr / bc1;
+  const AdamCoef c = adam_coef(lr, b1, b2, eps, wd, bc1, bc2_sqrt, hyper_dev);
   const long r0 = (long)blockIdx.y * 64, c0 = (long)blockIdx.x * 64;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
@@ -112,7 +137,7 @@ __global__ __launch_bounds__(256) void adamw_t_kernel(P* __restrict__ p, const P
     load8<P>(m + o, mv);
     load8<P>(v + o, vv);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) adamw_elem<FAST>(pv[j], mv[j], vv[j], gv[j], gs, decay, b1, b2, eps, bc2_sqrt, step_size);
+    for (int j = 0; j < 8; ++j) adamw_elem<FAST>(pv[j], mv[j], vv[j], gv[j], gs, c);
     store8<P>(p + o, pv);
     store8<P>(m + o, mv);
     store8<P>(v + o, vv);
@@ -170,9 +195,9 @@ __global__ __launch_bounds__(256) void norm_finish_kernel(const float* __restric
 extern "C" {
 
 // pdtype: param/grad dtype; sdtype: moment dtype
-hipError_t pra_adamw_flat(int pdtype, int sdtype, void* p, const void* g, void* m, void* v, long n, float lr,
-                          float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt, float gscale,
-                          const float* gscale_dev, const float* hyper_dev, int fast, hipStream_t s) {
+hipError_t pra_adamw_flat(int pdtype, int sdtype, void* p, const void* g, void* m, void* v, long n, double lr,
+                          double b1, double b2, double eps, double wd, double bc1, double bc2_sqrt, float gscale,
+                          const float* gscale_dev, const double* hyper_dev, int fast, hipStream_t s) {
   long blocks = (n / 8 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
@@ -193,9 +218,9 @@ hipError_t pra_adamw_flat(int pdtype, int sdtype, void* p, const void* g, void* 
 
 // AdamW of one [rows, cols] matrix + its transposed copy pt [cols, rows] (rows, cols % 64 == 0;
 // 16-bit params, moments of the same dtype).
-hipError_t pra_adamw_t(int dtype, void* p, const void* g, void* m, void* v, void* pt, int rows, int cols, float lr,
-                       float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt, float gscale,
-                       const float* gscale_dev, const float* hyper_dev, int fast, hipStream_t s) {
+hipError_t pra_adamw_t(int dtype, void* p, const void* g, void* m, void* v, void* pt, int rows, int cols, double lr,
+                       double b1, double b2, double eps, double wd, double bc1, double bc2_sqrt, float gscale,
+                       const float* gscale_dev, const double* hyper_dev, int fast, hipStream_t s) {
   if (rows % 64 || cols % 64 || rows <= 0 || cols <= 0) return hipErrorInvalidValue;
   // (A strip kernel walking 4 tiles per block was faster in isolation, 22.7 -> 21.3 ms per 7B step,
   // but slower overlapped with the backward GEMMs on the side stream: 1074.5 vs 1069.6 ms/step,

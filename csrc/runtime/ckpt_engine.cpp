@@ -56,7 +56,8 @@ void register_ckpt_engine(py::module& m) {
       .def("busy", &CkptEngine::busy)
       .def("flush", &CkptEngine::flush, py::call_guard<py::gil_scoped_release>())
       .def("md5_pending", &CkptEngine::md5_pending)
-      .def("abandon_md5", &CkptEngine::abandon_md5)
+      .def("abandon_md5", &CkptEngine::abandon_md5, py::call_guard<py::gil_scoped_release>())
+      .def("md5_max_seconds", &CkptEngine::md5_max_seconds)
       .def("wait", [](CkptEngine& e) {
         JobResult r;
         {

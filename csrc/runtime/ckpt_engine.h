@@ -489,7 +489,9 @@ class CkptEngine {
   // next 32 MiB read and is joined here, so no digest thread outlives the call (interpreter
   // shutdown, static destructors). A cancelled digest leaves no `.md5`; the `.md5parts` written
   // with the archive still verify it.
-  void abandon_md5() {
+  // Returns the error of a digest that had failed on its own before the cancel ("" if none): a
+  // cancelled digest records nothing, so what is left is a real failure.
+  std::string abandon_md5() {
     md5st_->cancel = true;
     std::vector<std::thread> th;
     {
@@ -498,8 +500,14 @@ class CkptEngine {
     }
     for (auto& t : th) t.join();
     std::lock_guard<std::mutex> g(md5st_->mu);
-    md5st_->error.clear();  // "cancelled" is not a failure
+    std::string e;
+    e.swap(md5st_->error);
     md5st_->cancel = false;  // later saves digest again
+    return e;
+  }
+  double md5_max_seconds() {
+    std::lock_guard<std::mutex> g(md5st_->mu);
+    return md5st_->max_seconds;
   }
   bool md5_pending() {
     std::lock_guard<std::mutex> g(md5st_->mu);
@@ -873,9 +881,14 @@ class CkptEngine {
     ::close(fd);
     if (!err.empty()) throw std::runtime_error(err);
     r.bytes = total;
-    if (want_md5 && (!whole_md5 || deferred)) ::unlink((path + ".md5").c_str());  // no stale digest
-    if (::rename(tmp.c_str(), path.c_str()) != 0)
-      throw std::runtime_error("ckpt_engine: rename failed: " + std::string(strerror(errno)));
+    {
+      // under the sidecar lock: an earlier deferred digest of the same path either wrote its
+      // sidecar before this unlink, or sees the new inode after the rename and writes nothing
+      std::lock_guard<std::mutex> g(sidecar_mu());
+      if (want_md5 && (!whole_md5 || deferred)) ::unlink((path + ".md5").c_str());  // no stale digest
+      if (::rename(tmp.c_str(), path.c_str()) != 0)
+        throw std::runtime_error("ckpt_engine: rename failed: " + std::string(strerror(errno)));
+    }
     if (want_md5) {
       // whole-file MD5 (the reference's `.md5` sidecar: 32 hex chars, no newline) and the
       // per-segment list
@@ -898,6 +911,8 @@ class CkptEngine {
     std::lock_guard<std::mutex> g(md5_th_mu_);
     md5_th_.emplace_back([st, path, do_fsync] {
       std::string err;
+      const auto t0 = std::chrono::steady_clock::now();
+      bool done = false;
       try {
         const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
         if (fd < 0) throw std::runtime_error("ckpt_engine: deferred md5: cannot open " + path);
@@ -914,18 +929,30 @@ class CkptEngine {
         // write the sidecar only if `path` is still the file that was hashed: retention may have
         // deleted it meanwhile (no orphan `.md5`), or a new save of the same path may have
         // replaced it (its own digest owns the sidecar; no false mismatch on resume)
+        // check and write under the lock a new save of the path takes around its unlink + rename
+        std::lock_guard<std::mutex> g(sidecar_mu());
         struct stat now {};
         if (::stat(path.c_str(), &now) == 0 && now.st_ino == before.st_ino && now.st_dev == before.st_dev &&
             now.st_mtim.tv_sec == before.st_mtim.tv_sec && now.st_mtim.tv_nsec == before.st_mtim.tv_nsec &&
             now.st_size == before.st_size)
           write_sidecar(path + ".md5", md5, do_fsync);
+        done = true;
       } catch (const std::exception& e) {
         if (!st->cancel.load()) err = e.what();
       }
+      const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       std::lock_guard<std::mutex> g2(st->mu);
       if (!err.empty()) st->error = err;
+      if (done) st->max_seconds = std::max(st->max_seconds, sec);
       --st->running;
     });
+  }
+
+  // Process-wide: orders a deferred digest's check-and-write of `<path>.md5` against a new save of
+  // the same path (every engine instance, every thread).
+  static std::mutex& sidecar_mu() {
+    static std::mutex mu;
+    return mu;
   }
 
   static void write_sidecar(const std::string& p, const std::string& text, bool do_fsync) {
@@ -949,6 +976,7 @@ class CkptEngine {
   struct Md5State {
     std::mutex mu;
     int running = 0;
+    double max_seconds = 0;  // longest completed deferred digest (feeds the time-aware budget)
     std::string error;
     std::atomic<bool> cancel{false};
   };

@@ -17,18 +17,19 @@ def native():
     global _C, _err
     if _C is not None:
         return _C
+    env = _attn_env()  # a malformed PYRECOVER_ATTN_* raises ValueError naming it, not a load error
     try:
         import torch  # noqa: F401  (loads torch's HIP runtime first; our .so binds to it)
         from pyrecover_amd import _C as mod
-        _C = mod
-        _apply_attn_env()
-        return _C
     except BaseException as e:  # pragma: no cover - exercised only when the build is missing
         _err = e
         raise RuntimeError(
             "pyrecover_amd native extension is not built or failed to load "
             f"({e!r}). Build it with `python -m pyrecover_amd._build` (hipcc --offload-arch=gfx950)."
         ) from e
+    _apply_options(mod, env)
+    _C = mod  # published only once the options applied
+    return _C
 
 
 def available() -> bool:
@@ -70,23 +71,34 @@ _ATTN_DEFAULTS = {"fwd_pipe": -1, "fwd_thr": 8.0, "dkdv_impl": -1, "dq_pipe": -1
 _attn_opts = dict(_ATTN_DEFAULTS)
 
 
-def _apply_attn_env():
+def _attn_env() -> dict:
     env = {}
     for key, conv in (("fwd_pipe", int), ("fwd_thr", float), ("dkdv_impl", int), ("dq_pipe", int)):
-        v = os.environ.get("PYRECOVER_ATTN_" + key.upper())
+        name = "PYRECOVER_ATTN_" + key.upper()
+        v = os.environ.get(name)
         if v is not None and v != "":
-            env[key] = conv(v)
-    set_attn_options(**env)
+            try:
+                env[key] = conv(v)
+            except ValueError:
+                raise ValueError(f"{name}={v!r} is not a valid {conv.__name__}") from None
+    return env
+
+
+def _apply_options(mod, env: dict) -> None:
+    opts = dict(_attn_opts)
+    opts.update(env)
+    mod.attn_set_options(opts["fwd_pipe"], opts["fwd_thr"], opts["dkdv_impl"], opts["dq_pipe"])
+    _attn_opts.update(opts)
 
 
 def set_attn_options(**kw) -> dict:
     """Set attention kernel selection knobs (fwd_pipe, fwd_thr, dkdv_impl, dq_pipe); keys left out
     keep their value, ``None`` restores the default. Returns the previous settings."""
     prev = dict(_attn_opts)
+    new = {}
     for k, v in kw.items():
         if k not in _ATTN_DEFAULTS:
             raise KeyError(f"unknown attention option {k!r}")
-        _attn_opts[k] = _ATTN_DEFAULTS[k] if v is None else type(_ATTN_DEFAULTS[k])(v)
-    _C.attn_set_options(_attn_opts["fwd_pipe"], _attn_opts["fwd_thr"], _attn_opts["dkdv_impl"],
-                        _attn_opts["dq_pipe"])
+        new[k] = _ATTN_DEFAULTS[k] if v is None else type(_ATTN_DEFAULTS[k])(v)
+    _apply_options(native(), new)
     return prev

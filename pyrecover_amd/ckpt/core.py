@@ -333,6 +333,12 @@ def max_write_seconds() -> float:
     return WRITE_STATS["max_seconds"]
 
 
+def max_digest_seconds() -> float:
+    """Longest completed deferred whole-file ``.md5`` digest of this process (0 if none yet): a
+    final checkpoint that computes its ``.md5`` inline takes about max(write, digest)."""
+    return max([c.engine.md5_max_seconds() for c in Checkpointer._instances.values()] + [0.0])
+
+
 def inflight_remaining(estimate: float) -> float:
     """Seconds the in-flight background writes still need, given an estimate of one full write."""
     now = time.perf_counter()
@@ -368,9 +374,14 @@ def abandon_deferred_md5():
     the job's wall-clock limit is near). A digest cut short leaves no ``.md5``; the ``.md5parts``
     written with the archive still verify the resume."""
     _FLUSH_AT_EXIT[0] = False
+    errors = []
     for c in list(Checkpointer._instances.values()):
         c.wait()
-        c.engine.abandon_md5()
+        e = c.engine.abandon_md5()  # a digest that failed on its own (not by the cancel)
+        if e:
+            errors.append(e)
+    if errors:  # reported, not raised: this runs on the way out of a preempted job
+        logger.error("deferred .md5 digest failed before it was abandoned: " + "; ".join(errors))
 
 
 def _flush_at_exit():

@@ -40,7 +40,10 @@ def _device_of(model) -> torch.device:
 def save_ckpt_vanilla(model, optimizer, lr_scheduler=None, sampler=None, step: int = 0, epoch: Optional[int] = None,
                       checkpoint_path: str = "checkpoint.pt", max_keep: int = 3, verify: bool = True,
                       is_distributed: bool = False, rank: int = 0, *, async_save: bool = False, fsync: bool = True,
-                      extra_state=None) -> str:
+                      extra_state=None, defer_md5: Optional[bool] = None) -> str:
+    """``defer_md5`` (default: on unless PYRECOVER_DEFER_MD5=0): with ``verify`` the whole-file
+    ``.md5`` is computed by a background re-read after the archive is durable; False computes it
+    inline, so the sidecar exists when the save returns (the time-aware final checkpoint)."""
     if is_distributed:
         dist.barrier()
     rngs = core.gather_rng_states() if is_distributed else None  # collective: every rank's streams
@@ -63,7 +66,9 @@ def save_ckpt_vanilla(model, optimizer, lr_scheduler=None, sampler=None, step: i
         # The archive and its .md5parts (parallel per-segment MD5s, what our loader verifies) are
         # durable when the job completes; the reference's whole-file .md5 (serial MD5 at ~0.9 GB/s,
         # ~45 s at 7B) follows from a background re-read of the file unless PYRECOVER_DEFER_MD5=0.
-        defer = verify and os.environ.get("PYRECOVER_DEFER_MD5", "1") != "0"
+        if defer_md5 is None:
+            defer_md5 = os.environ.get("PYRECOVER_DEFER_MD5", "1") != "0"
+        defer = verify and defer_md5
         ck.write(str(checkpoint_path), [("zip", records)], verify, fsync, (staged, keep), done, defer_md5=defer)
         if not async_save:
             ck.wait()

@@ -432,7 +432,7 @@ def _attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, causal, rope_tab=None) -> 
         _ext.require_for(q).attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, causal, rope_tab,
                                      ev.cuda_event if ev is not None else 0)
         if ev is not None:
-            sched.attention_window(ev)
+            sched.attention_window(ev, q.device.index)
         return rope_tab is not None
     ct = torch.promote_types(q.dtype, torch.float32)
     with torch.enable_grad():

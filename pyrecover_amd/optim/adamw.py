@@ -32,12 +32,17 @@ FUSED_T = os.environ.get("PRA_FUSED_ADAMW_T", "1") == "1"
 # Same-process A/B (profiles/r3/step_ab_attnwin_*.log): 7B B16 1063.3 -> 1056.5 ms, 7B B1 99.6 ->
 # 97.9 ms, Llama-3-8B S8192 B1 373.3 -> 361.5 ms, GPT-2-medium unchanged; no update at all: 1043.9
 # ms at B16. (Holding the updates for the W1|W3 / QKV data-gradient GEMMs instead measured +1.45%.)
+# Until a window has been seen, a bucket is held for at most one bucket: when the next bucket is
+# reduced and no attention window released the held ones (a model whose attention takes the torch
+# path -- fp64, head_dim not 64/128 -- or has no attention), they are enqueued then, so the update
+# still overlaps the backward instead of running serialized in step().
 OPT_SCHED = os.environ.get("PYRECOVER_OPT_SCHED", "attn")
-# PYRECOVER_ADAMW_FAST (default 1): hardware reciprocal / square root in the update
-# (csrc/kernels/optim.hip adamw_elem<FAST>: ~17 instead of ~60 VALU per element, which matters
-# beside the attention backward; 7B B1 98.5 -> 97.2 ms, B16 -0.15%, profiles/r3/step_ab_fast_*.log);
-# 0: torch _fused_adamw_'s correctly rounded divisions (p's update term differs by a few fp32 ulps)
-FAST_MATH = os.environ.get("PYRECOVER_ADAMW_FAST", "1") == "1"
+# PYRECOVER_ADAMW_FAST (default 0): torch _fused_adamw_'s exact expression tree (mixed fp64/fp32,
+# correctly rounded divisions; bit-equal to the reference's --fused-optimizer). 1: the
+# hardware reciprocal / square root in pure fp32 (csrc/kernels/optim.hip adamw_elem<FAST>, ~17
+# instead of ~60 VALU per element beside the attention backward; 7B B1 98.5 -> 97.2 ms, B16 within
+# noise, profiles/r3/step_ab_fast_*.log), whose p differs from torch's by a few fp32 ulps.
+FAST_MATH = os.environ.get("PYRECOVER_ADAMW_FAST", "0") == "1"
 
 
 class FlatAdamW(torch.optim.AdamW):
@@ -67,6 +72,7 @@ class FlatAdamW(torch.optim.AdamW):
         self._in_step = False
         self._done_ranges = []
         self._held = []  # (lo, hi, work) of reduced buckets not yet enqueued (OPT_SCHED "attn")
+        self._window_seen = False  # an attention window released held buckets (HIP attention path)
         self.pre_update_fences = []  # callables run on the update stream before any update
         # graph mode (train.py --compile): step-dependent scalars come from device memory
         self.graph_mode = False
@@ -76,16 +82,16 @@ class FlatAdamW(torch.optim.AdamW):
 
     # --- captured-step (HIP graph) support ---------------------------------------------------
     def enable_graph_mode(self):
-        """Kernels read {lr, bc1, bc2_sqrt} from ``self.hyper`` (device fp32[3]) instead of
+        """Kernels read {lr, bc1, bc2_sqrt} from ``self.hyper`` (device fp64[3]) instead of
         launch arguments, and the host step counter advances in :meth:`begin_graph_step`, so one
         captured step replays correctly at every later step and learning rate."""
         if not self.flat.data.is_cuda:
             raise RuntimeError("graph mode needs the parameters on a GPU")
         self.graph_mode = True
         dev = self.flat.data.device
-        self.hyper = torch.zeros(3, dtype=torch.float32, device=dev)
+        self.hyper = torch.zeros(3, dtype=torch.float64, device=dev)
         # pinned staging ring: a slot is rewritten only after its previous H2D copy completed
-        self._hyper_ring = [(torch.zeros(3, dtype=torch.float32).pin_memory(), torch.cuda.Event()) for _ in range(4)]
+        self._hyper_ring = [(torch.zeros(3, dtype=torch.float64).pin_memory(), torch.cuda.Event()) for _ in range(4)]
 
     def begin_graph_step(self):
         """Host side of one replayed step: advance the step count and upload the scalars."""
@@ -106,7 +112,8 @@ class FlatAdamW(torch.optim.AdamW):
         self.reducer = reducer
         reducer.hooks.append(self._on_bucket)
         self.stream = torch.cuda.Stream(device=self.flat.data.device) if self.flat.data.is_cuda else None
-        sched.add_attention_window_hook(self.release_held)
+        dev = self.flat.data.device
+        sched.add_attention_window_hook(self.release_held, dev.index if dev.type == "cuda" else None)
 
     def _coeffs(self):
         g = self.param_groups[0]
@@ -162,6 +169,10 @@ class FlatAdamW(torch.optim.AdamW):
             self._update_range(lo, hi)
             self._done_ranges.append((lo, hi))
             return
+        if self._held and not self._window_seen:
+            # no attention window has released held buckets yet: this model's backward may offer
+            # none, so do not wait any longer than one bucket
+            self.release_held()
         self._held.append((lo, hi, work))
         if OPT_SCHED != "attn":
             self.release_held()
@@ -170,6 +181,8 @@ class FlatAdamW(torch.optim.AdamW):
         """Enqueue the held bucket updates on the side stream behind `event` (default: one recorded
         on the compute stream now). Every read of their weights was enqueued before the bucket was
         published, so any later point of the compute stream is safe."""
+        if event is not None:
+            self._window_seen = True  # called from an attention window of this device
         if not self._held:
             return
         if event is None:

@@ -74,7 +74,9 @@ def gpu_index(lrank: int) -> int:
       one GPU; use with PYRECOVER_DIST_BACKEND=gloo).
     * One visible device (SLURM per-task isolation: ``--gpus-per-task=1`` / ``--gpu-bind``, or
       ROCR/HIP_VISIBLE_DEVICES set per rank): device 0, whatever SLURM_LOCALID says.
-    * Otherwise every node GPU is visible, as in reference dist_utils.py:47,55: ``lrank % count``.
+    * Otherwise every node GPU is visible, as in reference dist_utils.py:47,55: GPU ``lrank``. More
+      local ranks than visible GPUs is refused here (the reference's ``set_device`` fails loudly
+      too), instead of letting two ranks share a GPU and RCCL fail later with an unrelated error.
 
     ``torch.cuda.device_count()`` does not initialise the GPU on this image."""
     o = os.environ.get("PYRECOVER_LOCAL_DEVICE")
@@ -83,7 +85,15 @@ def gpu_index(lrank: int) -> int:
     n = torch.cuda.device_count() if torch.cuda.is_available() else 0
     if n <= 0:
         return lrank
-    return 0 if n == 1 else lrank % n
+    if n == 1:
+        return 0
+    if lrank >= n:
+        raise RuntimeError(
+            f"local rank {lrank} (SLURM_LOCALID={os.environ.get('SLURM_LOCALID')}, "
+            f"LOCAL_RANK={os.environ.get('LOCAL_RANK')}) has no GPU of its own: only {n} are visible. "
+            f"Launch at most {n} tasks per node, bind one GPU per task, or set PYRECOVER_LOCAL_DEVICE "
+            f"to share one deliberately")
+    return lrank
 
 
 def rccl_pg_options():

@@ -98,6 +98,49 @@ class _StepTimer:
         return longest
 
 
+class _StopFlagSync:
+    """Rank 0's stop decision broadcast to every rank without a per-step host sync.
+
+    The reference broadcasts ``should_stop`` and calls ``.item()`` at the end of every step
+    (train.py:343-346), which drains the device queue each step. Here the
+    broadcast of step t is enqueued asynchronously, its result is copied into pinned host memory
+    behind an event, and it is read at the end of step t+1: every rank acts on the same broadcast,
+    one step later, and the host keeps one step of run-ahead. The time-aware threshold budgets
+    6 iterations (reference train.py:304), so the extra step fits."""
+
+    def __init__(self, device: torch.device):
+        self.cuda = device.type == "cuda"
+        self.dev = torch.zeros(1, dtype=torch.int32, device=device)
+        self.host = torch.zeros(1, dtype=torch.int32, pin_memory=self.cuda)
+        self.pending = None
+
+    def collect(self) -> bool:
+        """Result of the previously posted broadcast (False when none is pending)."""
+        if self.pending is None:
+            return False
+        work, ev = self.pending
+        self.pending = None
+        if ev is not None:
+            ev.synchronize()
+            return bool(self.host[0])
+        work.wait()
+        return bool(self.dev[0])
+
+    def post(self, flag: bool) -> bool:
+        """Collect the previous step's decision, then broadcast this step's; returns the former."""
+        prev = self.collect()
+        self.dev.fill_(1 if flag else 0)
+        work = torch.distributed.broadcast(self.dev, src=0, async_op=True)
+        ev = None
+        if self.cuda:
+            work.wait()  # the current stream waits for the collective; the host does not
+            self.host.copy_(self.dev, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        self.pending = (work, ev)
+        return prev
+
+
 def train(args):
     training_start_time = time.perf_counter()
     total_checkpoint_store_time = 0.0
@@ -132,6 +175,12 @@ def train(args):
         vocab = args.vocab_size or tokenizer.vocab_size
         pad_id = tokenizer.pad_token_id
     log_rank0(f"Global batch size: {global_batch_size}\nLocal batch size: {local_batch_size}")
+    if local_batch_size * world_size != global_batch_size:
+        # reference train.py:62-63 keeps max(B//W,1) per rank but counts B·S tokens per step
+        # (:252); here throughput counts what actually runs
+        log_rank0(f"Note: --batch-size {global_batch_size} is not a multiple of world size {world_size}: "
+                  f"each step runs {local_batch_size} x {world_size} = {local_batch_size * world_size} "
+                  f"sequences, and tokens/s counts those")
     if accum > 1:
         log_rank0(f"Gradient accumulation: {accum} micro-batches per step "
                   f"({global_batch_size * accum} sequences per optimizer step)")
@@ -234,9 +283,15 @@ def train(args):
     def do_save(step, epoch, final=False):
         p = ckpt_name(step, final)
         t0 = time.perf_counter()
+        kw = {}
+        if final and not args.use_torch_distributed_ckpt:
+            # the final (time-aware) checkpoint computes its whole-file .md5 inline, so the sidecar
+            # the reference's verified load requires (pyrecover/checkpoint.py:157-175) exists when
+            # the save returns; the stop threshold budgets that digest (max_digest_seconds)
+            kw["defer_md5"] = False
         save_ckpt_fn(model, optimizer, lr_scheduler, train_sampler, step, epoch, p,
                      max_keep=args.max_kept_checkpoints, verify=args.verify_checkpoints, is_distributed=is_dist,
-                     rank=rank, async_save=(args.async_checkpoint and not final), fsync=not args.no_fsync)
+                     rank=rank, async_save=(args.async_checkpoint and not final), fsync=not args.no_fsync, **kw)
         if final:
             ckcore.wait_all()
             if args.use_torch_distributed_ckpt:
@@ -277,7 +332,7 @@ def train(args):
     train_dl_iterator = iter(train_dl)
     should_stop = False
     stopped_for_time = False
-    stop_flag = torch.zeros(1, dtype=torch.int32, device=device)
+    stop_sync = _StopFlagSync(device) if (stopper is not None and is_dist) else None
     log_rank0("Starting training!")
     if world_size > 1:
         print(f"[Rank {rank}] Starting training on {device}", flush=True)
@@ -289,8 +344,12 @@ def train(args):
             # drains the in-flight write: budget full write times
             ckcore.poll_all()
             wsec = ckcore.max_write_seconds()
+            if args.verify_checkpoints and not args.use_torch_distributed_ckpt:
+                # the final save's inline whole-file digest runs beside its write (serial MD5,
+                # ~0.9 GB/s): budget the longer of the two, as measured on earlier saves
+                wsec = max(wsec, ckcore.max_digest_seconds())
             if stopper.update_ckpt(wsec):
-                log_rank0(f"Updated max_ckpt_time from background write time: {stopper.max_ckpt:.2f}")
+                log_rank0(f"Updated max_ckpt_time from background write/digest time: {stopper.max_ckpt:.2f}")
             stopper.inflight_drain = ckcore.inflight_remaining(stopper.max_ckpt)
         if stopper is not None and D.is_rank0() and stopper.should_stop():
             should_stop = True
@@ -315,7 +374,8 @@ def train(args):
                 input_ids, labels = next(train_dl_iterator)
             train_sampler.advance(input_ids.shape[0])
 
-            ntokens_since_last_log += global_batch_size * seq_len
+            # true tokens of this step on all ranks (every rank runs the same local batch)
+            ntokens_since_last_log += input_ids.shape[0] * world_size * seq_len
             num_items_in_batch = labels.ne(-100).sum()
             ntraining_tokens_since_last_log += int(num_items_in_batch) * world_size
             micro.append((input_ids.to(device, non_blocking=True), labels.to(device, non_blocking=True)))
@@ -389,9 +449,8 @@ def train(args):
             log_rank0(f"Checkpoint store completed in {store_time:.2f} seconds")
 
         if stopper is not None and is_dist:
-            stop_flag.fill_(1 if (should_stop or stopper.signaled) else 0)
-            torch.distributed.broadcast(stop_flag, src=0)
-            should_stop = bool(stop_flag.item())
+            # rank 0's decision of the previous step (no per-step host sync)
+            should_stop = stop_sync.post(should_stop or stopper.signaled)
         elif stopper is not None and stopper.signaled:
             should_stop = True
 
@@ -417,6 +476,8 @@ def train(args):
     # drain background checkpoint writes (and deferred .md5 digests) before reporting; after a
     # time-aware stop the digests get only the time left before the wall-clock limit (minus a
     # margin; 60 s after a signal) -- one cut short leaves no .md5, and .md5parts verify the resume
+    if stop_sync is not None:
+        stop_sync.collect()  # retire the last posted broadcast before teardown
     t0 = time.perf_counter()
     ckcore.wait_all()
     finalize_pending()

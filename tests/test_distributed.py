@@ -108,19 +108,43 @@ def _worker_slurm(rank, world, port, argv, out_dir, end_in_s):
 
 def test_fake_slurm_two_ranks_timeaware_stop_and_resume(tmp_path):
     """2 gloo ranks bootstrapped from fake SLURM variables (SLURM_PROCID/NTASKS/LOCALID) and
-    a SLURM_JOB_END_TIME 30 s away: both ranks agree to stop after step 1 (stop flag broadcast from rank
-    0), write the final sharded checkpoint, and a second fake-SLURM job resumes it to completion."""
+    a SLURM_JOB_END_TIME 30 s away: rank 0 decides to stop at step 1, its flag (broadcast without a
+    per-step host sync, read one step later: SURVEY D16) stops both ranks after step 2, they write
+    the final sharded checkpoint, and a second fake-SLURM job resumes it to completion."""
     ck = tmp_path / "ck"
     argv = _argv(ck, 6, ["--distributed", "--use-torch-distributed-ckpt", "--timeaware-checkpointing",
                          "--checkpoint-frequency", "-1"])
     mp.spawn(_worker_slurm, args=(2, _free_port(), argv, str(tmp_path), 30.0), nprocs=2, join=True)
     r0 = torch.load(tmp_path / "res_0.pt", weights_only=False)
     r1 = torch.load(tmp_path / "res_1.pt", weights_only=False)
-    assert r0["stopped_early"] and r1["stopped_early"] and r0["step"] == r1["step"] == 1
-    assert (ck / "e" / "ckpt_1_final" / ".metadata").exists()
+    assert r0["stopped_early"] and r1["stopped_early"] and r0["step"] == r1["step"] == 2
+    assert (ck / "e" / "ckpt_2_final" / ".metadata").exists()
     argv2 = _argv(ck, 3, ["--distributed", "--use-torch-distributed-ckpt", "--resume-from-checkpoint", "latest"])
     mp.spawn(_worker_slurm, args=(2, _free_port(), argv2, str(tmp_path), None), nprocs=2, join=True)
     assert torch.load(tmp_path / "res_0.pt", weights_only=False)["step"] == 3
+
+
+@pytest.mark.parametrize("batch", [1, 3])
+def test_tokens_per_second_counts_what_runs(tmp_path, batch):
+    """with --batch-size not a multiple of W the reference logs B·S tokens per step
+    (train.py:252) while each rank runs max(B//W,1) sequences (:62-63). Here the logged tokens/s
+    must match the tokens that actually ran (local 1 x W 2 x S) over the measured step time."""
+    import json
+
+    ck = tmp_path / "ck"
+    seq = 128
+    jl = tmp_path / "m.jsonl"
+    argv = _argv(ck, 8, ["--distributed", "--checkpoint-frequency", "-1", "--logging-frequency", "1",
+                         "--metrics-jsonl", str(jl)])
+    argv[argv.index("--batch-size") + 1] = str(batch)
+    _run(2, argv, tmp_path)
+    recs = [json.loads(ln) for ln in open(jl)]
+    assert [r["step"] for r in recs] == list(range(1, 9))
+    per_step = 1 * 2 * seq  # local batch max(B//2,1) = 1 on each of 2 ranks
+    ratios = sorted(r["tokens_per_s"] * (r["time"] - p["time"]) / per_step for p, r in zip(recs[1:], recs[2:]))
+    med = ratios[len(ratios) // 2]
+    assert 0.9 < med < 1.1, ratios
+    assert all(abs(r["tokens_per_s_per_gpu"] * 2 - r["tokens_per_s"]) < 1e-6 * r["tokens_per_s"] for r in recs)
 
 
 def _bench_json(out: str) -> dict:

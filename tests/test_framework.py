@@ -118,6 +118,42 @@ def test_timeaware_training_stops_and_resumes(tmp_path, monkeypatch):
     assert r["step"] == 3 and not r["stopped_early"]
 
 
+def test_timeaware_final_checkpoint_carries_md5_and_budgets_digest(tmp_path, monkeypatch):
+    """The time-aware final checkpoint is written with its whole-file .md5 (inline, not a deferred
+    digest that the wall-clock limit may cut short), and the stop threshold budgets the digest time
+    measured on earlier saves. Checked with the reference's own verification logic
+    (pyrecover/checkpoint.py:157-171: md5 of the whole file == the sidecar's text)."""
+    import hashlib
+
+    from pyrecover_amd.ckpt import core as ckcore
+    from pyrecover_amd.cli import get_args
+    from pyrecover_amd.trainer import train
+
+    end = time.time() + 300  # far above the initial 41 s threshold ...
+    monkeypatch.setenv("SLURM_JOB_END_TIME", str(end))
+    # ... until the first save reports a 400 s whole-file digest (a big model's serial MD5)
+    monkeypatch.setattr(ckcore, "max_digest_seconds",
+                        lambda: 400.0 if ckcore.WRITE_STATS["max_seconds"] > 0 else 0.0)
+    monkeypatch.setitem(ckcore.WRITE_STATS, "max_seconds", 0.0)
+    monkeypatch.setattr(ckcore, "_FLUSH_AT_EXIT", [True])  # abandon_deferred_md5 clears it
+
+    def limit_reached(deadline=None):  # every deferred digest still running is abandoned
+        ckcore.abandon_deferred_md5()
+        return False
+
+    monkeypatch.setattr(ckcore, "flush_all", limit_reached)
+    args = ["--model-preset", "llama-micro", "--synthetic-data", "--sequence-length", "128", "--batch-size", "2",
+            "--training-steps", "50", "--checkpoint-dir", str(tmp_path), "--checkpoint-frequency", "2",
+            "--model-dtype", "fp32", "--num-workers", "0", "--timeaware-checkpointing", "--verify-checkpoints"]
+    r = train(get_args(args))
+    assert r["stopped_early"] and r["step"] == 3, r
+    final = tmp_path / "default-exp" / "ckpt_3_final.pt"
+    side = Path(str(final) + ".md5")
+    assert side.exists() and side.stat().st_mtime < end
+    with open(final, "rb") as f:
+        assert hashlib.md5(f.read()).hexdigest() == side.read_text()
+
+
 def test_slurm_duration_parse_and_remaining(monkeypatch):
     from pyrecover_amd.timelimit import _parse_slurm_duration, get_remaining_time
 

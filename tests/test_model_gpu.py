@@ -130,6 +130,49 @@ def test_optimizer_schedules_are_bit_identical(cuda, monkeypatch, sched):
     assert torch.equal(p0, p1) and torch.equal(v0, v1)
 
 
+def test_overlap_without_hip_attention_updates_during_backward(cuda):
+    """head_dim 32 takes the torch attention path, which offers no attention window: the default
+    OPT_SCHED "attn" must not hold every bucket until step() (which would serialize the update
+    after the backward), but enqueue them during the backward; results equal the plain step."""
+    from pyrecover_amd.config import TransformerModelArgs
+    from pyrecover_amd.ops import sched
+    from pyrecover_amd.optim.adamw import FlatAdamW
+    from pyrecover_amd.parallel.ddp import GradReducer
+
+    a = TransformerModelArgs(dim=256, n_layers=2, n_heads=8, n_kv_heads=8, multiple_of=64, vocab_size=512,
+                             seq_len=128)
+    out = []
+    for overlap in (False, True):
+        torch.manual_seed(0)
+        prev = torch.get_default_dtype()
+        torch.set_default_dtype(torch.bfloat16)
+        with torch.device(cuda):
+            m = Transformer(a)
+        torch.set_default_dtype(prev)
+        flat = m.flatten_()
+        red = GradReducer(flat, bucket_cap_mb=0.25, first_bucket_mb=0.125)
+        opt = FlatAdamW(flat, lr=1e-3)
+        if overlap:
+            opt.enable_overlap(red)
+        g = torch.Generator(device=cuda)
+        g.manual_seed(7)
+        during = []
+        for _ in range(2):
+            t = torch.randint(0, a.vocab_size, (2, 129), device=cuda, generator=g)
+            opt.zero_grad()
+            w0 = sched.windows_fired()
+            m(t[:, :-1], labels=t[:, 1:]).backward()
+            assert sched.windows_fired() == w0  # torch attention path: no window offered
+            during.append(len(opt._done_ranges))
+            red.finish()
+            opt.step()
+        torch.cuda.synchronize()
+        out.append((flat.data.clone(), opt.exp_avg_sq.clone()))
+        if overlap:
+            assert red.num_buckets > 3 and min(during) >= red.num_buckets - 2, (during, red.num_buckets)
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+
+
 def test_activation_checkpointing_is_bit_identical(cuda):
     """Recomputing each block in backward (with the overlapped per-bucket update running) gives
     the same parameters and moments as keeping the activations."""

@@ -154,9 +154,12 @@ def test_two_task_slurm_launch_binds_and_trains(tmp_path):
     assert "Starting training!" in txt
 
 
-@pytest.mark.parametrize("count,lrank,want", [(1, 3, 0), (8, 3, 3), (4, 5, 1), (0, 2, 2)])
+@pytest.mark.parametrize("count,lrank,want", [(1, 3, 0), (8, 3, 3), (8, 7, 7), (4, 5, None), (2, 2, None),
+                                              (0, 2, 2)])
 def test_gpu_index_maps_to_a_visible_device(monkeypatch, count, lrank, want):
-    """SLURM per-task isolation shows ONE device (index 0) whatever SLURM_LOCALID is."""
+    """SLURM per-task isolation shows ONE device (index 0) whatever SLURM_LOCALID is; with every
+    GPU visible a local rank gets its own GPU, and more local ranks than GPUs is refused (two
+    ranks silently sharing a GPU would fail later inside RCCL)."""
     import torch
 
     from pyrecover_amd.parallel import dist as D
@@ -165,6 +168,10 @@ def test_gpu_index_maps_to_a_visible_device(monkeypatch, count, lrank, want):
     monkeypatch.setenv("SLURM_LOCALID", str(lrank))
     monkeypatch.setattr(torch.cuda, "is_available", lambda: count > 0)
     monkeypatch.setattr(torch.cuda, "device_count", lambda: count)
-    assert D.gpu_index(lrank) == want
+    if want is None:
+        with pytest.raises(RuntimeError, match="has no GPU of its own"):
+            D.gpu_index(lrank)
+    else:
+        assert D.gpu_index(lrank) == want
     monkeypatch.setenv("PYRECOVER_LOCAL_DEVICE", "0")
     assert D.gpu_index(lrank) == 0
