@@ -52,6 +52,9 @@ hipError_t pra_gemm_nt(int dtype, int epi, const void* A, const void* B, void* C
                        float* ws, int* tickets, int cus, hipStream_t s);
 long pra_gemm_nt_ws_floats(int M, int N, int K, int cus);
 int pra_gemm_nt_ticket_count(int M, int N, int K, int cus);
+// main loop of K % 64 == 0 NT GEMMs: 1 = two-buffer schedule (default), 0 = the round-3 ring (A/B)
+void pra_gemm_nt_set_sched(int v);
+int pra_gemm_nt_sched();
 
 hipError_t pra_xent_fwd(int dtype, const void* logits, const int64_t* labels, float* lse, float* loss_row,
                         float* stats, long T, long V, long ld, long ignore_index, hipStream_t s);

@@ -74,8 +74,10 @@ __device__ __forceinline__ void adamw_elem(float& p, float& m, float& v, float g
     p = (float)fma(-c.lr_wd, pd, pd);
     m = (float)fma(c.b1, (double)m, (1.0 - c.b1) * gd);
     v = (float)fma(c.b2, (double)v, ((1.0 - c.b2) * gd) * gd);
-    const float denom = (float)((double)__fdiv_rn(__fsqrt_rn(v), c.bc2f) + c.eps);
-    p = p - __fdiv_rn(c.step_size * m, denom);
+    // sqrtf / '/' as ATen writes them (std::sqrt, operator/): correctly rounded under hipcc's default
+    // -fhip-fp32-correctly-rounded-divide-sqrt; __fsqrt_rn measured 1 ulp low on 0.08% of elements
+    const float denom = (float)((double)(sqrtf(v) / c.bc2f) + c.eps);
+    p = p - (c.step_size * m) / denom;
   }
 }
 

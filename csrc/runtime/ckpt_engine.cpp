@@ -17,10 +17,14 @@ void register_ckpt_engine(py::module& m) {
       .def("pool_ptr", &CkptEngine::pool_ptr)
       .def("pool_size", &CkptEngine::pool_size)
       .def("stage",
-           [](CkptEngine& e, const std::vector<std::pair<uintptr_t, uint64_t>>& regions) {
+           [](CkptEngine& e, const std::vector<std::pair<uintptr_t, uint64_t>>& regions, uintptr_t hbm,
+              uint64_t hbm_bytes) {
              const int dev = e.device();
-             return e.stage(regions, dev >= 0 ? c10::hip::getCurrentHIPStream(dev).stream() : nullptr);
-           })
+             return e.stage(regions, dev >= 0 ? c10::hip::getCurrentHIPStream(dev).stream() : nullptr, hbm,
+                            hbm_bytes);
+           },
+           py::arg("regions"), py::arg("hbm") = 0, py::arg("hbm_bytes") = 0)
+      .def("last_two_hop", &CkptEngine::last_two_hop)
       .def("fence",
            [](CkptEngine& e) {
              const int dev = e.device();

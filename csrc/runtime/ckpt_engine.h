@@ -341,6 +341,7 @@ class CkptEngine {
     release_chunks();
     free_pool();
     if (device_ >= 0) {
+      if (hbm_ev_ != nullptr) (void)hipEventDestroy(hbm_ev_);
       (void)hipEventDestroy(entry_ev_);
       (void)hipStreamDestroy(stream_);
     }
@@ -368,7 +369,13 @@ class CkptEngine {
   // Enqueue D2H copies of (dev_ptr, nbytes) regions into the pool, packed at 64-B aligned
   // offsets. Returns the host offsets. Ordered after all work already queued on `cur` (the
   // caller's compute stream; ignored in CPU mode).
-  std::vector<uint64_t> stage(const std::vector<std::pair<uintptr_t, uint64_t>>& regions, hipStream_t cur) {
+  //
+  // hbm (device pointer, hbm_bytes >= the packed size): two-hop snapshot. The regions are first
+  // copied device-to-device into this HBM buffer (tens of ms at HBM bandwidth); fence() waits for
+  // THAT copy only, and the slow D2H into the pinned pool (~0.6 s for 38 GiB) then drains from the
+  // HBM copy while the next optimizer steps overwrite the live buffers.
+  std::vector<uint64_t> stage(const std::vector<std::pair<uintptr_t, uint64_t>>& regions, hipStream_t cur,
+                              uintptr_t hbm = 0, uint64_t hbm_bytes = 0) {
     wait_writer();  // the pool is reused: the previous archive must be fully written
     release_chunks();
     uint64_t total = 0;
@@ -398,9 +405,20 @@ class CkptEngine {
     hip_check(hipSetDevice(device_), "hipSetDevice");
     hip_check(hipEventRecord(entry_ev_, cur), "event record");
     hip_check(hipStreamWaitEvent(stream_, entry_ev_, 0), "stream wait");
+    const bool two_hop = hbm != 0 && hbm_bytes >= total;
+    if (two_hop) {
+      for (size_t i = 0; i < regions.size(); ++i)
+        hip_check(hipMemcpyAsync((uint8_t*)hbm + offs[i], (const void*)regions[i].first, regions[i].second,
+                                 hipMemcpyDeviceToDevice, stream_),
+                  "hipMemcpyAsync D2D");
+      if (hbm_ev_ == nullptr) hip_check(hipEventCreateWithFlags(&hbm_ev_, hipEventDisableTiming), "event create");
+      hip_check(hipEventRecord(hbm_ev_, stream_), "event record");
+    }
+    fence_ev_ = two_hop ? hbm_ev_ : nullptr;  // null: the last D2H chunk
+    last_two_hop_ = two_hop;
     constexpr uint64_t kChunk = 256ull << 20;
     for (size_t i = 0; i < regions.size(); ++i) {
-      const uint8_t* src = (const uint8_t*)regions[i].first;
+      const uint8_t* src = two_hop ? (const uint8_t*)hbm + offs[i] : (const uint8_t*)regions[i].first;
       uint8_t* dst = (uint8_t*)pool_ + offs[i];
       for (uint64_t o = 0; o < regions[i].second; o += kChunk) {
         const uint64_t n = std::min(kChunk, regions[i].second - o);
@@ -419,8 +437,9 @@ class CkptEngine {
   // next optimizer step cannot overwrite parameters that are still being copied out.
   void fence(hipStream_t cur) {
     if (device_ < 0 || chunks_.empty()) return;
-    hip_check(hipStreamWaitEvent(cur, chunks_.back().ev, 0), "fence");
+    hip_check(hipStreamWaitEvent(cur, fence_ev_ != nullptr ? fence_ev_ : chunks_.back().ev, 0), "fence");
   }
+  bool last_two_hop() const { return last_two_hop_; }
   // Host-side: block until the snapshot has fully landed in host memory.
   void sync_stage() {
     if (!chunks_.empty()) hip_check(hipEventSynchronize(chunks_.back().ev), "event sync");
@@ -968,6 +987,9 @@ class CkptEngine {
   int device_;
   hipStream_t stream_ = nullptr;
   hipEvent_t entry_ev_ = nullptr;
+  hipEvent_t hbm_ev_ = nullptr;    // the D2D hop of a two-hop snapshot landed in the HBM buffer
+  hipEvent_t fence_ev_ = nullptr;  // what fence() waits for (null: the last D2H chunk)
+  bool last_two_hop_ = false;
   void* pool_ = nullptr;
   uint64_t pool_size_ = 0;
   uint64_t staged_bytes_ = 0;

@@ -188,6 +188,7 @@ class Checkpointer:
         self.pending: Optional["Job"] = None
         self.staged = False
         self._prewarm: Optional[threading.Thread] = None
+        self._hbm: Optional[torch.Tensor] = None
 
     def prewarm(self, nbytes: int, background: bool = True):
         """Allocate the pinned staging pool ahead of the first checkpoint. Prefer
@@ -235,7 +236,9 @@ class Checkpointer:
         total = sum(r[1] for r in regions) + 64 * len(regions)
         if total > self.engine.pool_size():
             self.engine.reserve(int(total * 1.05) + (1 << 20))
-        offs = self.engine.stage([(r[0], r[1]) for r in regions]) if regions else []
+        hbm = self._hbm_buffer(total) if (dev_is_cuda and regions) else None
+        offs = (self.engine.stage([(r[0], r[1]) for r in regions], hbm.data_ptr() if hbm is not None else 0,
+                                  hbm.numel() if hbm is not None else 0) if regions else [])
         base = self.engine.pool_ptr()
         starts = [r[0] for r in regions]
         import bisect
@@ -251,8 +254,30 @@ class Checkpointer:
         self.staged = True
         return _walk(obj, to_host)
 
+    def _hbm_buffer(self, nbytes: int) -> Optional[torch.Tensor]:
+        """Device-side bounce buffer of the two-hop snapshot: the live buffers are
+        copied into it at HBM bandwidth, the next update is fenced only on that copy, and the D2H
+        into the pinned pool drains from it. Kept across saves (one allocation); None -- direct
+        D2H as before -- when PYRECOVER_CKPT_HBM=0 or free HBM would drop below the reserve
+        (PYRECOVER_CKPT_HBM_RESERVE_GB, default 8) after allocating it."""
+        if os.environ.get("PYRECOVER_CKPT_HBM", "1") == "0":
+            return None
+        if self._hbm is not None and self._hbm.numel() >= nbytes:
+            return self._hbm
+        dev = torch.device("cuda", self.device_index)
+        self._hbm = None  # the previous snapshot was fully drained (stage() waited for the writer)
+        free, _ = torch.cuda.mem_get_info(dev)
+        reserve = float(os.environ.get("PYRECOVER_CKPT_HBM_RESERVE_GB", "8")) * 2**30
+        if free - nbytes < reserve:
+            logger.info(f"checkpoint snapshot: {nbytes / 2**30:.1f} GiB HBM bounce buffer does not fit "
+                        f"({free / 2**30:.1f} GiB free): direct D2H, the next update waits for it")
+            return None
+        self._hbm = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        return self._hbm
+
     def fence(self):
-        """Make the current compute stream wait (GPU-side) for the in-flight snapshot."""
+        """Make the current compute stream wait (GPU-side) for the in-flight snapshot: with the HBM
+        bounce buffer, for its device-to-device copy only."""
         if self.staged and self.device_index >= 0:
             self.engine.fence()
 
