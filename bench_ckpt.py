@@ -146,8 +146,11 @@ def main():
         out["async_stall_s"] = round(time.perf_counter() - t0, 3)
         t1 = time.perf_counter()
         step()  # training continues while the snapshot drains and the file is written
-        torch.cuda.synchronize()
+        # the compute stream only: a device-wide synchronize would also wait for the snapshot's
+        # D2H drain on the checkpoint engine's own stream, which training never waits for
+        torch.cuda.current_stream(dev).synchronize()
         out["async_overlapped_step_s"] = round(time.perf_counter() - t1, 3)
+        out["async_snapshot_two_hop"] = bool(core.Checkpointer.get(dev).engine.last_two_hop())
         core.wait_all()
         out["async_total_s"] = round(time.perf_counter() - t0, 3)
         os.remove(p)

@@ -772,8 +772,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("grad_norm", &grad_norm);
   m.def("wgrad_mm_", &wgrad_mm_);
   m.def("wgrad_mm_exp_", &wgrad_mm_exp_);
-  m.def("gemm_nt_set_sched", [](int64_t v) { pra_gemm_nt_set_sched((int)v); });
-  m.def("gemm_nt_sched", []() { return (int64_t)pra_gemm_nt_sched(); });
   m.def("gemm_nt_", &gemm_nt_, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("epi") = 0,
         py::arg("out2") = py::none(), py::arg("tab") = py::none(), py::arg("S") = 0, py::arg("D") = 0,
         py::arg("nrot") = 0);

@@ -18,7 +18,12 @@
 //
 // Deterministic (fixed summation order), so resumed runs stay bit-identical.
 // Requires M % 256 == 0, N % 256 == 0, K % 32 == 0, 16-B aligned rows (host-checked).
-// Measured history (32x32x16 MFMA, 4-stage ring, ...): profiles/wgrad_mfma_r2.md.
+// Measured history (32x32x16 MFMA, 4-stage ring, ...): profiles/wgrad_mfma_r2.md. Round 4: the
+// two-buffer 64-deep-chunk schedule that lifted the NT kernel +6-7% (gemm_nt.hip run2b) ran this
+// kernel 3-6% SLOWER than the 5-stage ring (1.32-1.45 vs 1.40-1.49 PF; profiles/r4/
+// wgrad_two_buffer_vs_ring.log; the cause was not isolated -- each fragment here is two
+// ds_read_b64_tr_b16, so a chunk boundary carries 32 outstanding LDS reads per k-substep, more than
+// the 4-bit lgkmcnt can count); removed.
 #include "gemm_common.h"
 
 #include <stdlib.h>

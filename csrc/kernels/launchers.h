@@ -52,9 +52,6 @@ hipError_t pra_gemm_nt(int dtype, int epi, const void* A, const void* B, void* C
                        float* ws, int* tickets, int cus, hipStream_t s);
 long pra_gemm_nt_ws_floats(int M, int N, int K, int cus);
 int pra_gemm_nt_ticket_count(int M, int N, int K, int cus);
-// main loop of K % 64 == 0 NT GEMMs: 1 = two-buffer schedule (default), 0 = the round-3 ring (A/B)
-void pra_gemm_nt_set_sched(int v);
-int pra_gemm_nt_sched();
 
 hipError_t pra_xent_fwd(int dtype, const void* logits, const int64_t* labels, float* lse, float* loss_row,
                         float* stats, long T, long V, long ld, long ignore_index, hipStream_t s);
@@ -68,6 +65,8 @@ int pra_sumsq_partials();
 hipError_t pra_grad_norm(int dtype, const void* x, long n, float* ws, float* out, float max_norm, float pre_scale,
                          hipStream_t s);
 
+// dst <- src, nbytes, device memory (16-B vector path when both are 16-B aligned)
+hipError_t pra_copy_d2d(void* dst, const void* src, long nbytes, hipStream_t s);
 hipError_t pra_sum_slices(int dtype, const void* const* srcs, int nsrc, void* dst, long n, hipStream_t s);
 
 hipError_t pra_adamw_t(int dtype, void* p, const void* g, void* m, void* v, void* pt, int rows, int cols, double lr,

@@ -21,6 +21,10 @@
 #pragma once
 #include <hip/hip_runtime_api.h>
 
+// the bandwidth-bound D2D copy kernel of csrc/kernels/comm.hip (linked into pyrecover_amd._C); weak,
+// so the host-only engine self-test links without the kernels (it never takes the device path)
+extern "C" hipError_t pra_copy_d2d(void* dst, const void* src, long nbytes, hipStream_t s) __attribute__((weak));
+
 #include <openssl/evp.h>
 #include <zlib.h>
 #include <immintrin.h>
@@ -407,10 +411,14 @@ class CkptEngine {
     hip_check(hipStreamWaitEvent(stream_, entry_ev_, 0), "stream wait");
     const bool two_hop = hbm != 0 && hbm_bytes >= total;
     if (two_hop) {
-      for (size_t i = 0; i < regions.size(); ++i)
-        hip_check(hipMemcpyAsync((uint8_t*)hbm + offs[i], (const void*)regions[i].first, regions[i].second,
-                                 hipMemcpyDeviceToDevice, stream_),
-                  "hipMemcpyAsync D2D");
+      for (size_t i = 0; i < regions.size(); ++i) {
+        void* d = (uint8_t*)hbm + offs[i];
+        const void* sp = (const void*)regions[i].first;
+        if (pra_copy_d2d != nullptr)
+          hip_check(pra_copy_d2d(d, sp, (long)regions[i].second, stream_), "snapshot D2D copy");
+        else
+          hip_check(hipMemcpyAsync(d, sp, regions[i].second, hipMemcpyDeviceToDevice, stream_), "snapshot D2D copy");
+      }
       if (hbm_ev_ == nullptr) hip_check(hipEventCreateWithFlags(&hbm_ev_, hipEventDisableTiming), "event create");
       hip_check(hipEventRecord(hbm_ev_, stream_), "event record");
     }

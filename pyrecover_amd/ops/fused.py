@@ -198,10 +198,11 @@ def _wgrad_into(slot, dy2, x2, shape, site, force=False):
 # both operands K-contiguous (activations [T, in] x weights [out, in]; the data gradients use the
 # transposed weight shadows), with fused epilogues where a separate memory-bound pass followed:
 # RoPE on the QKV projection, SwiGLU on the W1|W3 projection, the SwiGLU backward on the W2 data
-# gradient. The kernel runs at 0.85-0.88 of hipBLASLt on the 7B shapes (1.35-1.40 vs 1.55-1.64
-# PF), which the fused epilogues do not win back (W1|W3 + SwiGLU 4.52 vs 4.09 ms, W2 data grad +
-# SwiGLU backward 2.77 vs 2.49 ms; profiles/gemm_nt_r3.md), so "auto" keeps every NT site on
-# hipBLASLt. PYRECOVER_GEMM: "auto" (default), "hip" (every valid site on the NT kernel), "lib",
+# gradient. With round 4's two-buffer main loop the kernel runs at 0.90-0.94 of hipBLASLt on the
+# 7B shapes (1.38-1.49 vs 1.53-1.63 PF; steady state 1.51 vs 1.65 PF, profiles/r4/), and in the
+# whole step the fused epilogues still do not win it back (7B B16: W1|W3 + SwiGLU +0.7%, W2 data
+# grad + SwiGLU backward +1.0%, both + QKV/RoPE +2.1% ms/step; profiles/r4/
+# step_ab_fused_epilogues.log), so "auto" keeps every NT site on hipBLASLt. PYRECOVER_GEMM: "auto" (default), "hip" (every valid site on the NT kernel), "lib",
 # or a comma list of sites: forward qkv, o, w13, w2, head; data gradient qkv_d, o_d, w13_d, w2_d,
 # head_d.
 _NT_ALL = frozenset({"qkv", "o", "w13", "w2", "head", "qkv_d", "o_d", "w13_d", "w2_d", "head_d"})

@@ -45,7 +45,6 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--cases", default="plain,swiglu,swiglu_b,rope")
     ap.add_argument("--shapes", default="")
-    ap.add_argument("--sched-ab", action="store_true", help="also time the round-3 main loop (sched 0)")
     args = ap.parse_args()
     from pyrecover_amd.utils.gemm_tuning import configure_gemm_tuning
 
@@ -92,18 +91,6 @@ def main():
             y2 = torch.empty_like(y)
 
             arms = {"lib": lambda: torch.mm(x, w.t(), out=y2), "hip": lambda: C.gemm_nt_(x, w, y)}
-            if args.sched_ab:
-                dflt = C.gemm_nt_sched()
-
-                def with_sched(v):
-                    def f():
-                        C.gemm_nt_set_sched(v)
-                        C.gemm_nt_(x, w, y)
-                        C.gemm_nt_set_sched(dflt)
-                    return f
-                for v in (0, 1, 2):
-                    if v != dflt:
-                        arms[f"hip_s{v}"] = with_sched(v)
             run_arms(name, 2.0 * T * N * K, arms, {"rel_err": round(err, 5)})
             del x, w, y, y2
             torch.cuda.empty_cache()

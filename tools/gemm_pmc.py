@@ -2,7 +2,7 @@
 
     python tools/gemm_pmc.py --kernel nt|nt32|wgrad|lib --m 32768 --n 12288 --k 4096 [--iters 5]
 
-nt/nt6/nt32: C.gemm_nt_ (x [m, k], w [n, k]); wgrad: C.wgrad_mm_ (dy [k, m]^T x [k, n], i.e. M=m);
+nt/nt32: C.gemm_nt_ (x [m, k], w [n, k]); wgrad: C.wgrad_mm_ (dy [k, m]^T x [k, n], i.e. M=m);
 lib: torch.mm(x, w.t()). Random uniform [-1, 1) bf16 operands."""
 import argparse
 import os
@@ -27,14 +27,12 @@ def main():
     configure_gemm_tuning("auto")  # lib: the step's tuned hipBLASLt solution table
     C = _ext.native()
     dev = torch.device("cuda", 0)
-    if a.kernel == "nt6":  # the round-3 main loop (5-unit ring)
-        C.gemm_nt_set_sched(0)
 
     def rnd(*s):
         return (torch.rand(*s, device=dev) * 2 - 1).bfloat16()
     if a.kernel == "nt32":
         os.environ["PRA_GEMM_NT_KB"] = "32"
-    if a.kernel in ("nt", "nt6", "nt32", "lib"):
+    if a.kernel.startswith("nt") or a.kernel == "lib":
         x, w = rnd(a.m, a.k), rnd(a.n, a.k) * 0.05
         y = torch.empty(a.m, a.n, device=dev, dtype=torch.bfloat16)
         f = (lambda: torch.mm(x, w.t(), out=y)) if a.kernel == "lib" else (lambda: C.gemm_nt_(x, w, y))
