@@ -73,6 +73,12 @@ def launch_command(argv, gpus: int, env) -> list:
             "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + list(argv)
 
 
+def _adamw_fast() -> bool:
+    from pyrecover_amd.optim import adamw
+
+    return adamw.FAST_MATH
+
+
 def _opt_sched() -> str:
     from pyrecover_amd.optim import adamw
 
@@ -131,7 +137,7 @@ def main():
         torch.set_default_dtype(torch.bfloat16)
         model = Transformer(cfg)
         torch.set_default_dtype(prev)
-    flat = model.flatten_()
+    flat = model.flatten_(tokens_per_step=args.batch_per_gpu * args.seq_len)
     if world > 1:
         broadcast_flat(flat)
     reducer = GradReducer(flat, bucket_cap_mb=args.bucket_mb, backend=args.allreduce)
@@ -250,7 +256,9 @@ def main():
                        "grad_buckets": reducer.num_buckets,
                        "rccl_high_priority_stream": os.environ.get("PYRECOVER_RCCL_HIGH_PRIORITY", "1") == "1",
                        "optimizer": "AdamW (flat fused HIP)" + ("" if args.no_overlap_optimizer else
-                                                                 f", overlapped with backward ({_opt_sched()})")},
+                                                                 f", overlapped with backward ({_opt_sched()})"),
+                       "adamw_math": "hw rcp/sqrt (fast)" if _adamw_fast() else "torch _fused_adamw_ bit-exact",
+                       "weight_shadows": bool(getattr(flat, "t_mats", None))},
             "tokens_per_sec_per_gpu": round(tps / world, 2),
             "model_tflops_per_gpu": round(fpt * tps / world / 1e12, 2),
             "mfu_pct_vs_2.5PF": round(100 * fpt * tps / world / 2.5e15, 2),

@@ -27,6 +27,9 @@ from ..ops.reference import precompute_freqs_cis, rope_table
 from ..parallel.flat import FlatParams
 
 
+
+SHADOW_MIN_TOKENS = 8192  # see Transformer.flatten_
+
 class RMSNorm(nn.Module):
     """Parameter container + reference-compatible eager forward (reference model.py:25-49)."""
 
@@ -197,14 +200,24 @@ class Transformer(nn.Module):
         g.append([("output.weight", self.output.weight)])
         return g
 
-    def flatten_(self) -> FlatParams:
-        """Move all parameters/gradients into flat buffers (call after the final .to(device/dtype))."""
+    def flatten_(self, tokens_per_step: Optional[int] = None) -> FlatParams:
+        """Move all parameters/gradients into flat buffers (call after the final .to(device/dtype)).
+
+        Transposed weight shadows (K-contiguous W^T for the data-gradient GEMMs, rewritten by the
+        optimizer) pay off when the GEMMs are large: +3.5% at 7B B16 (profiles/ab_weight_shadows_s7.log),
+        but at 2048 tokens per step the 2 B/param they add to the update traffic costs more than
+        the faster dgrad layout returns (Llama-3-8B B1: 107.5 vs 108.7 ms/step without them,
+        profiles/r4/). So they are kept from SHADOW_MIN_TOKENS tokens per micro-step (or when the
+        count is unknown); PRA_WEIGHT_SHADOWS=1/0 forces them on/off."""
         if self.flat is None:
             self.flat = FlatParams(self.fusion_groups())
             # optimizer-state indices follow model.parameters() order, as in the reference
             self.flat.module_order = list(self.parameters())
-            # PRA_WEIGHT_SHADOWS=0 drops the transposed copies (dgrad GEMMs then read W as stored)
-            shadows = os.environ.get("PRA_WEIGHT_SHADOWS", "1") != "0"
+            env = os.environ.get("PRA_WEIGHT_SHADOWS", "")
+            if env in ("0", "1"):
+                shadows = env == "1"
+            else:
+                shadows = tokens_per_step is None or tokens_per_step >= SHADOW_MIN_TOKENS
             for mats in self._gemm_weights() if shadows else []:
                 self.flat.register_transposed(mats, (sum(p.shape[0] for p in mats), mats[0].shape[1]))
             # parameters written through the module API must refresh the transposed shadows

@@ -198,7 +198,7 @@ def train(args):
     with set_default_dtype(model_dtype), torch.device(device):
         model = Transformer(model_config)
     model.activation_checkpointing = bool(getattr(args, "activation_checkpointing", False))
-    flat = model.flatten_()
+    flat = model.flatten_(tokens_per_step=local_batch_size * seq_len)
     overlap = not (args.clip_grad or args.no_overlap_optimizer)
     reducer = None
     if is_dist:

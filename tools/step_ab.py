@@ -72,7 +72,7 @@ def main():
         torch.set_default_dtype(torch.bfloat16)
         model = Transformer(cfg)
         torch.set_default_dtype(prev)
-    flat = model.flatten_()
+    flat = model.flatten_(tokens_per_step=a.batch_per_gpu * a.seq_len)
     reducer = GradReducer(flat, bucket_cap_mb=256.0)
     opt = FlatAdamW(flat, lr=1e-5, fused=True)
     opt.enable_overlap(reducer)
