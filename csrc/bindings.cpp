@@ -718,7 +718,8 @@ void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, con
     at::Tensor lp = at::zeros({B, Hq, Sp}, lse.options());
     lp.narrow(2, 0, S).copy_(lse.view({B, Hq, S}));
     at::Tensor dqp = at::empty_like(qp), dkp = at::empty_like(kp), dvp = at::empty_like(vp);
-    at::Tensor delta = at::empty({3, B, Hq, Sp}, q.options().dtype(at::kFloat));  // see pra_attn_bwd
+    at::Tensor delta = at::empty({pra_attn_bwd_workspace(dt(q), (int)B, (int)Sp, (int)Hq, (int)Hkv, (int)D)},
+                                 q.options().dtype(at::kFloat));
     check(pra_attn_bwd(dt(q), qp.data_ptr(), kp.data_ptr(), vp.data_ptr(), op.data_ptr(), dop.data_ptr(),
                        lp.data_ptr<float>(), delta.data_ptr<float>(), dqp.data_ptr(), dkp.data_ptr(), dvp.data_ptr(),
                        (int)B, (int)Sp, (int)Hq, (int)Hkv, (int)D, qp.stride(1), kp.stride(1), vp.stride(1),
@@ -730,7 +731,8 @@ void attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, con
     dv.copy_(dvp.narrow(1, 0, S));
     return;
   }
-  at::Tensor delta = at::empty({3, B, Hq, S}, q.options().dtype(at::kFloat));  // see pra_attn_bwd
+  at::Tensor delta = at::empty({pra_attn_bwd_workspace(dt(q), (int)B, (int)S, (int)Hq, (int)Hkv, (int)D)},
+                               q.options().dtype(at::kFloat));
   check(pra_attn_bwd(dt(q), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
                      lse.data_ptr<float>(), delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
                      (int)B, (int)S, (int)Hq, (int)Hkv, (int)D, q.stride(1), k.stride(1), v.stride(1), o.stride(1),
@@ -784,9 +786,11 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("dout"), pybind11::arg("lse"), pybind11::arg("dq"), pybind11::arg("dk"), pybind11::arg("dv"),
         pybind11::arg("scale"), pybind11::arg("causal"), pybind11::arg("rope_tab") = pybind11::none(),
         pybind11::arg("mid_event") = 0);
-  m.def("attn_set_options", [](int fwd_pipe, double fwd_thr, int dkdv_impl, int dq_pipe) {
-    pra_attn_set_options(fwd_pipe, (float)fwd_thr, dkdv_impl, dq_pipe);
-  }, "attention kernel selection: fwd_pipe / dkdv_impl / dq_pipe = -1 (by shape), 0 or 1; fwd_thr = rescale threshold (log2)");
+  m.def("attn_set_options", [](int fwd_pipe, double fwd_thr, int dkdv_impl, int dq_pipe, int dkdv_split, int dkdv_kreg) {
+    pra_attn_set_options(fwd_pipe, (float)fwd_thr, dkdv_impl, dq_pipe, dkdv_split, dkdv_kreg);
+  }, "attention kernel selection: fwd_pipe / dkdv_impl / dq_pipe = -1 (by shape), 0 or 1; fwd_thr = rescale "
+     "threshold (log2); dkdv_split = -1 (by grid) or query-head splits of the pipelined dK/dV kernel; "
+     "dkdv_kreg = 1: two-wave dK/dV kernel keeps K in registers");
   register_ckpt_engine(m);
   register_xgmi(m);
 }

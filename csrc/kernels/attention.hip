@@ -140,6 +140,35 @@ __device__ __forceinline__ void store_rows16(const f32x16 (&acc)[NDB], float f, 
     }
 }
 
+// store_rows16's register layout written as fp32 (no lane exchange): the lane's 4-column groups
+// sit at 32 db + 16 m + 4 h2 (registers 8m..8m+3) and 8 further on (8m+4..8m+7)
+template <int NDB>
+__device__ __forceinline__ void store_rows16_f32(const f32x16 (&acc)[NDB], float f, float* p, int h2,
+                                                 const float2* rt = nullptr) {
+#pragma unroll
+  for (int db = 0; db < NDB; ++db)
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int a = 8 * m, c = 8 * m + 4;
+      float va[4], vc[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        va[j] = acc[db][a + j] * f;
+        vc[j] = acc[db][c + j] * f;
+      }
+      if (rt != nullptr) {
+        const float4 ta = *reinterpret_cast<const float4*>(rt + 16 * db + 8 * m + 2 * h2);
+        const float4 tc = *reinterpret_cast<const float4*>(rt + 16 * db + 8 * m + 4 + 2 * h2);
+        rot_inv(va[0], va[1], ta.x, ta.y);
+        rot_inv(va[2], va[3], ta.z, ta.w);
+        rot_inv(vc[0], vc[1], tc.x, tc.y);
+        rot_inv(vc[2], vc[3], tc.z, tc.w);
+      }
+      *reinterpret_cast<float4*>(p + 32 * db + 16 * m + 4 * h2) = make_float4(va[0], va[1], va[2], va[3]);
+      *reinterpret_cast<float4*>(p + 32 * db + 16 * m + 8 + 4 * h2) = make_float4(vc[0], vc[1], vc[2], vc[3]);
+    }
+}
+
 // lanes i and i^32 exchange through v_permlane32_swap (no LDS round trip)
 __device__ __forceinline__ float half_max(float x) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
@@ -634,7 +663,9 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const T* __restrict__
 // NW = 4 (128 keys, 80 KB, two blocks per CU): the constants arrive as one float per lane and are
 // broadcast with ds_bpermute (no LDS left for them).
 // ======================================================================================
-template <typename T, int D, bool CAUSAL, int NW>
+// KREG (NW = 8 only): the wave's K row fragments (32 VGPRs at D = 128) are read from LDS once and
+// kept in registers, cutting the per-tile LDS reads from 48 to 40 KB per wave.
+template <typename T, int D, bool CAUSAL, int NW, bool KREG = false>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
     const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V,
     const T* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
@@ -713,6 +744,12 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
       c8 = v8;
     }
   }
+  static_assert(!KREG || ROWC_LDS, "KREG reads the prescaled K image of the NW = 8 kernel");
+  V8<T> kf[KREG ? NKS : 1];
+  if constexpr (KREG) {
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) kf[ks] = lo.rowk(Kw, 0, ks);  // the wave's own rows (rescaled above)
+  }
 
   for (int it = 0; it < total; ++it) {
     const int hq = hk * nrep + it / nqt;
@@ -748,7 +785,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
         }
       }
       // S chain then dP chain: one operand pair in flight ahead of each MFMA
-      V8<T> xa = lo.rowk(Qs, 0, 0), xb = lo.rowk(Kw, 0, 0);
+      V8<T> xa = lo.rowk(Qs, 0, 0), xb = KREG ? kf[0] : lo.rowk(Kw, 0, 0);
 #pragma unroll
       for (int st = 0; st < 2 * NKS; ++st) {
         const int ks = st % NKS;
@@ -756,7 +793,10 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
         if (st + 1 < 2 * NKS) {
           const int nks = (st + 1) % NKS;
           na = lo.rowk(st + 1 < NKS ? Qs : Ds, 0, nks);
-          nb = lo.rowk(st + 1 < NKS ? Kw : Vw, 0, nks);
+          if (KREG && st + 1 < NKS)
+            nb = kf[KREG ? nks : 0];
+          else
+            nb = lo.rowk(st + 1 < NKS ? Kw : Vw, 0, nks);
         }
         if (st < NKS) s = mfma(xa, xb, s);
         else dp = mfma(xa, xb, dp);
@@ -837,7 +877,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
     const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V,
     const T* __restrict__ dO, const float* __restrict__ NLS, const float* __restrict__ NDelta,
     T* __restrict__ dK, T* __restrict__ dV, int S, int Hq, int Hkv, long ldq, long ldk, long ldv,
-    long lddo, long lddk, long lddv, float scale, float scale_log2, int skv, const float2* __restrict__ rtab) {
+    long lddo, long lddk, long lddv, float scale, float scale_log2, int skv, const float2* __restrict__ rtab,
+    int nsplit, float* __restrict__ part) {
   constexpr int NW = 4, KB = 32 * NW, QS = 64;
   constexpr int NKS = D / 16, NDB = D / 32;
   constexpr int KVT = KB * D, QDT = QS * D;
@@ -851,9 +892,12 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
   const int nkb = S / KB;
   const int BH = gridDim.x / nkb;
   const int kbk = (int)(blockIdx.x / BH);  // causal: early key blocks have the most work
-  const int bh = blockIdx.x % BH;
-  const int hk = bh % Hkv, b = bh / Hkv;
-  const int nrep = Hq / Hkv;
+  const int bh = blockIdx.x % BH;  // (b, kv head, split)
+  const int sp = bh % nsplit, hk = (bh / nsplit) % Hkv, b = bh / (nsplit * Hkv);
+  // split > 1: the block covers nrep of the kv head's Hq / Hkv query heads and leaves fp32 partial
+  // dK/dV in `part` for dkdv_reduce_kernel (small grids: see dkdv_split)
+  const int nrep = (Hq / Hkv) / nsplit;
+  const int hq0 = hk * (Hq / Hkv) + sp * nrep;
   const int k0 = kbk * KB, kw = k0 + wid * 32;
 
   GStage<T, D, QS, NW> gq, gd;
@@ -863,7 +907,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
   const int nqs = (S - qstart) / QS;
   const int total = nqs * nrep;
   auto issue_step = [&](int t, int buf) {
-    const int hq = hk * nrep + t / nqs;
+    const int hq = hq0 + t / nqs;
     const int q0 = qstart + (t % nqs) * QS;
     gq.issue(Q + ((long)b * S + q0) * ldq + hq * D, smem + buf * 2 * QDT);
     gd.issue(dO + ((long)b * S + q0) * lddo + hq * D, smem + buf * 2 * QDT + QDT);
@@ -1009,9 +1053,34 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void bwd_dkdv_p2_kernel(
 
   const int krow = kw + l32;
   // rtab: inverse RoPE on dK (table rows = positions; padded rows >= skv are discarded, clamp them)
-  store_rows16<T, NDB>(dkt, scale, dK + ((long)b * S + krow) * lddk + hk * D, true, h2,
-                       rtab ? rtab + (long)min(krow, skv - 1) * (D / 2) : nullptr);
-  store_rows16<T, NDB>(dvt, 1.f, dV + ((long)b * S + krow) * lddv + hk * D, true, h2);
+  const float2* rt = rtab ? rtab + (long)min(krow, skv - 1) * (D / 2) : nullptr;
+  if (part == nullptr) {
+    store_rows16<T, NDB>(dkt, scale, dK + ((long)b * S + krow) * lddk + hk * D, true, h2, rt);
+    store_rows16<T, NDB>(dvt, 1.f, dV + ((long)b * S + krow) * lddv + hk * D, true, h2);
+  } else {  // [split][dK, dV][B][S][Hkv][D] fp32 (scale and inverse RoPE are linear: applied per part)
+    const long n = (long)(BH / nsplit) * S * D;
+    float* pk = part + (long)sp * 2 * n + ((long)b * S + krow) * Hkv * D + hk * D;
+    store_rows16_f32<NDB>(dkt, scale, pk, h2, rt);
+    store_rows16_f32<NDB>(dvt, 1.f, pk + n, h2);
+  }
+}
+
+// dK, dV = sum of the split dK/dV kernel's fp32 parts (fixed order: deterministic), cast to T
+template <typename T>
+__global__ __launch_bounds__(256) void dkdv_reduce_kernel(const float* __restrict__ part, int nsplit, long n, int hd,
+                                                          T* __restrict__ dK, long lddk, T* __restrict__ dV,
+                                                          long lddv) {
+  const long e = ((long)blockIdx.x * 256 + threadIdx.x) * 4;  // n % 4 == 0, hd % 4 == 0
+  if (e >= 2 * n) return;
+  float4 a = *reinterpret_cast<const float4*>(part + e);
+  for (int j = 1; j < nsplit; ++j) {
+    const float4 c = *reinterpret_cast<const float4*>(part + (long)j * 2 * n + e);
+    a.x += c.x; a.y += c.y; a.z += c.z; a.w += c.w;
+  }
+  const bool isv = e >= n;
+  const long r = isv ? e - n : e, tok = r / hd;
+  T* dst = (isv ? dV + tok * lddv : dK + tok * lddk) + (r - tok * hd);
+  *reinterpret_cast<uint2*>(dst) = make_uint2(pack_x2<T>(a.x, a.y), pack_x2<T>(a.z, a.w));
 }
 
 // ======================================================================================
@@ -1251,6 +1320,12 @@ struct AttnOptions {
   int dkdv_impl = -1;
   // dQ: -1/1 = region-pipelined bwd_dq_kernel<PIPE>, 0 = plain (padded non-causal keys: always plain)
   int dq_pipe = -1;
+  // pipelined dK/dV kernel, query heads per block: -1 = by grid size (dkdv_split), 1 = all of the
+  // kv head's Hq / Hkv heads in one block, n = Hq / Hkv / n heads per block plus an fp32 reduction
+  int dkdv_split = -1;
+  // two-wave dK/dV kernel (NW = 8, D = 128): 1 = K fragments held in registers (KREG), 0 = read from LDS
+  // (B16 S2048 H32 bwd 2.387 -> 2.358 ms: profiles/r4/attn_ab_dkdv_kreg_b16.log)
+  int dkdv_kreg = 1;
 };
 AttnOptions g_attn_opts;
 
@@ -1290,6 +1365,34 @@ static bool dkdv_use_p2(int B, int S, int Hq, int Hkv, int D) {
   const int impl = g_attn_opts.dkdv_impl;
   const long grid2 = (long)(S / 256) * Hkv * B;
   return impl == 1 || (impl < 0 && (D == 64 || ((long)(Hq / Hkv) * S >= 8192 && grid2 <= 256)));
+}
+
+// GQA at small batch: the pipelined dK/dV grid is (S / 128) Hkv B blocks, one per CU at D = 128
+// (Llama-3-8B B1 S2048 bwd 0.297 -> 0.206 (2 splits) -> 0.172 ms (4); S8192: 1.717 ms unsplit, the
+// best: profiles/r4/attn_ab_dkdv_split_*.log)
+// -- 128 blocks (half the chip) for Llama-3-8B B1 S2048 H32/8, and the causal work per block falls
+// 16:1 from the first key block to the last. Splitting the kv head's query heads over n blocks gives
+// n times the grid; with the heavy key blocks dispatched first, a CU that drew a light block picks
+// up the next one, so two rounds of blocks even out to ~ (S/128 + 1) / 2 steps of work per CU. The
+// price is an fp32 partial per split and one reduction pass (2 n B S Hkv D floats).
+static int dkdv_split(int B, int S, int Hq, int Hkv, int D) {
+  const int nrep = Hq / Hkv;
+  int n = g_attn_opts.dkdv_split;
+  if (n < 0) {
+    const long grid = (long)(S / 128) * Hkv * B, want = D == 64 ? 1024 : 512;
+    n = 1;
+    while (grid * n < want && nrep % (2 * n) == 0) n *= 2;
+  }
+  return (n >= 1 && nrep % n == 0) ? n : 1;
+}
+
+// fp32 workspace of pra_attn_bwd, in floats: delta, the row constants (-lse log2(e), -delta) of the
+// pipelined dK/dV kernel, and its split partials
+long attn_bwd_ws_floats(int B, int S, int Hq, int Hkv, int D) {
+  const long nrc = (long)B * Hq * S;
+  const bool p2 = dkdv_use_p2(B, S, Hq, Hkv, D);
+  const int n = p2 ? dkdv_split(B, S, Hq, Hkv, D) : 1;
+  return 3 * nrc + (n > 1 ? 2L * n * B * S * Hkv * D : 0);
 }
 
 template <typename T>
@@ -1335,21 +1438,31 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
   }
   if (mid_event != nullptr) hipEventRecord(mid_event, st);  // between the dQ and dK/dV launches
   if (p2) {
-    dim3 g1((S / 128) * Hkv * B);
+    const int ns = dkdv_split(B, S, Hq, Hkv, D);
+    float* part = ns > 1 ? delta + 3 * nrc : nullptr;  // attn_bwd_ws_floats
+    dim3 g1((S / 128) * Hkv * B * ns);
 #define LAUNCH1(DD, CC)                                                                                       \
   hipLaunchKernelGGL((bwd_dkdv_p2_kernel<T, DD, CC>), g1, dim3(256), 0, st, (const T*)q, (const T*)k,        \
                      (const T*)v, (const T*)dout, rc2, rc2 + nrc, (T*)dk, (T*)dv, S, Hq, Hkv, ldq, ldk, ldv,   \
-                     lddo, lddk, lddv, scale, sl2, skv, rt)
+                     lddo, lddk, lddv, scale, sl2, skv, rt, ns, part)
     if (D == 128) { if (causal) LAUNCH1(128, true); else LAUNCH1(128, false); }
     else { if (causal) LAUNCH1(64, true); else LAUNCH1(64, false); }
 #undef LAUNCH1
+    if (ns > 1) {
+      const long n = (long)B * S * Hkv * D;
+      hipLaunchKernelGGL((dkdv_reduce_kernel<T>), dim3((unsigned)((2 * n / 4 + 255) / 256)), dim3(256), 0, st,
+                         (const float*)part, ns, n, Hkv * D, (T*)dk, lddk, (T*)dv, lddv);
+    }
   } else {
     dim3 grid((S / (32 * nw)) * Hkv * B);
-#define LAUNCH(DD, CC, NWW)                                                                                     \
-  hipLaunchKernelGGL((bwd_dkdv_kernel<T, DD, CC, NWW>), grid, dim3(NWW * 64), 0, st, (const T*)q, (const T*)k, \
+#define LAUNCH(DD, CC, NWW, ...)                                                                                \
+  hipLaunchKernelGGL((bwd_dkdv_kernel<T, DD, CC, NWW, ##__VA_ARGS__>), grid, dim3(NWW * 64), 0, st, (const T*)q,   \
+                     (const T*)k,                                                                               \
                      (const T*)v, (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Hq, Hkv, ldq, ldk, ldv, lddo,  \
                      lddk, lddv, scale, sl2, skv, rt)
-    if (nw == 8) {
+    if (nw == 8 && D == 128 && g_attn_opts.dkdv_kreg == 1) {
+      if (causal) LAUNCH(128, true, 8, true); else LAUNCH(128, false, 8, true);
+    } else if (nw == 8) {
       if (D == 128) { if (causal) LAUNCH(128, true, 8); else LAUNCH(128, false, 8); }
       else { if (causal) LAUNCH(64, true, 8); else LAUNCH(64, false, 8); }
     } else {
@@ -1401,11 +1514,18 @@ hipError_t pra_attn_bwd(int dtype, const void* q, const void* k, const void* v, 
 }
 
 // Kernel selection (see AttnOptions); not thread-safe against concurrent launches (set between steps).
-void pra_attn_set_options(int fwd_pipe, float fwd_thr, int dkdv_impl, int dq_pipe) {
+void pra_attn_set_options(int fwd_pipe, float fwd_thr, int dkdv_impl, int dq_pipe, int dkdv_split, int dkdv_kreg) {
   g_attn_opts.fwd_pipe = fwd_pipe;
   g_attn_opts.fwd_thr = fwd_thr;
   g_attn_opts.dkdv_impl = dkdv_impl;
   g_attn_opts.dq_pipe = dq_pipe;
+  g_attn_opts.dkdv_split = dkdv_split;
+  g_attn_opts.dkdv_kreg = dkdv_kreg;
+}
+
+long pra_attn_bwd_workspace(int dtype, int B, int S, int Hq, int Hkv, int D) {
+  if (dtype == pra::kF32) return 3L * B * Hq * S;
+  return attn_bwd_ws_floats(B, S, Hq, Hkv, D);
 }
 
 }  // extern "C"

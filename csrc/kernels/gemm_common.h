@@ -43,6 +43,13 @@ __device__ __forceinline__ void dma16s(const void* sbase, uint32_t voff, uint32_
                : "memory");
 }
 
+// The same DMA as two statements, for schedules that put an MFMA between the M0 write and the load
+// (the MFMA is the wait state, so no s_nop): m0_set, >= 1 other instruction, dma16s_go.
+__device__ __forceinline__ void m0_set(uint32_t lds) { asm volatile("s_mov_b32 m0, %0" ::"s"(lds)); }
+__device__ __forceinline__ void dma16s_go(const void* sbase, uint32_t voff) {
+  asm volatile("global_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase) : "memory");
+}
+
 // s_waitcnt vmcnt(N) for a compile-time N
 template <int N>
 __device__ __forceinline__ void wait_vm() {

@@ -65,6 +65,43 @@ __device__ __forceinline__ void unpack4(uint2 w, float (&o)[4]) {
   for (int e = 0; e < 4; ++e) o[e] = (float)h[e];
 }
 
+// Diagnostic build only (tools/nt_stamps.hip defines PRA_NT_STAMPS): per-wave s_memtime sums of the
+// two-buffer loop's phases, written once per wave at the end of the tile. The stamps sit where
+// lgkmcnt is already 0 (after the phase-1 drain, after each barrier, before the vmcnt wait), so
+// the counted LDS waits are unchanged.
+#ifdef PRA_NT_STAMPS
+__device__ unsigned long long* pra_nt_stamp_out;
+#define PRA_NT_STAMP(v)                  \
+  do {                                   \
+    __builtin_amdgcn_sched_barrier(0);   \
+    v = __builtin_amdgcn_s_memtime();    \
+    __builtin_amdgcn_sched_barrier(0);   \
+  } while (0)
+#else
+#define PRA_NT_STAMP(v) \
+  do {                  \
+  } while (0)
+#endif
+
+#ifndef PRA_NT_P1
+#define PRA_NT_P1 32
+#endif
+#ifndef PRA_NT_RS1
+#define PRA_NT_RS1 1
+#endif
+#ifndef PRA_NT_P3
+#define PRA_NT_P3 16
+#endif
+#ifndef PRA_NT_RS3
+#define PRA_NT_RS3 1
+#endif
+// M0SPLIT 1: 1432-1449 vs 1429-1431 TF without (32768x4096x4096; per-chunk phase 2 1467 vs 1515
+// cycles); spreading the fragment reads one per two or three MFMAs (RS > 1) was 2-9% slower:
+// profiles/r4/gemm_nt_schedule_variants*.log
+#ifndef PRA_NT_M0SPLIT
+#define PRA_NT_M0SPLIT 1
+#endif
+
 // the XOR swizzle of the 16-B chunk of row r: g((r >> 2) & 3), g = {0, 2, 3, 1}
 __device__ __forceinline__ int swz(int r) {
   const int q = (r >> 2) & 3;
@@ -276,53 +313,98 @@ __global__ __launch_bounds__(NTH) void gemm_nt_kernel(const T* __restrict__ A, c
       else
         acc[i][j] = mfma16(fb1[j], fa1[i], acc[i][j]);
     };
+#ifdef PRA_NT_STAMPS
+    unsigned long long ts1, ts2, ts3, ts4, ts4p = 0, sw1 = 0, sp2 = 0, sw2 = 0, sp31 = 0, nch = 0;
+#endif
+    // schedule knobs (defaults: the production schedule; tools/nt_stamps.hip builds variants):
+    // P1 / P3 MFMAs in phases 1 / 3, one fragment read per RS1 / RS3 MFMAs, phase 2 = the rest with
+    // the 16 DMAs spread evenly; M0SPLIT puts one MFMA between each DMA's M0 write and its load
+    constexpr int P1 = PRA_NT_P1, RS1 = PRA_NT_RS1, P3 = PRA_NT_P3, RS3 = PRA_NT_RS3;
+    constexpr int MD = (128 - P1 - P3) / 16;
+    static_assert(P1 >= 16 * RS1 && P3 >= 16 * RS3 && P3 <= 64 && (128 - P1 - P3) % 16 == 0 && MD >= 2,
+                  "NT schedule knobs");
+    auto dma_lds = [&](int b, int d) __attribute__((always_inline)) {
+      return ldsw + (uint32_t)((b * 2 + (d >> 3)) * TILE64 * sizeof(T) + (d & 7) * 4 * 1024);
+    };
+    auto dma_go = [&](int c, int d) __attribute__((always_inline)) {
+      c = min(c, c1 - 1);
+      const int i = d & 7;
+      if (d >= 8)
+        dma16s_go(Bb + (long)row_b64(i) * ldb + (long)c * 64, vob64);
+      else
+        dma16s_go(Ab + (long)row_a64(i) * lda + (long)c * 64, voa64);
+    };
     auto chunk = [&](auto b_c, int t) __attribute__((always_inline)) {
       constexpr int b = decltype(b_c)::value;
-      // phase 1: MFMA 0..31; k-substep-1 fragments of chunk t under the first 16
+      // phase 1: MFMA 0..P1-1; k-substep-1 fragments of chunk t (B first: MFMA 64..71 need fb1[0..7])
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        mf(q);
-        if (q < 8)
-          fb1[q] = fragB(b, 1, q);
+      for (int r = 0; r < 16; ++r) {
+#pragma unroll
+        for (int k = 0; k < RS1; ++k) mf(r * RS1 + k);
+        if (r < 8)
+          fb1[r] = fragB(b, 1, r);
         else
-          fa1[q - 8] = fragA(b, 1, q - 8);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          fa1[r - 8] = fragA(b, 1, r - 8);
+        __builtin_amdgcn_sched_group_barrier(0x008, RS1, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
 #pragma unroll
-      for (int q = 16; q < 32; ++q) mf(q);
-      __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+      for (int q = 16 * RS1; q < P1; ++q) mf(q);
+      if constexpr (P1 > 16 * RS1) __builtin_amdgcn_sched_group_barrier(0x008, P1 - 16 * RS1, 0);
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0), visible to the compiler's wait counting
+      PRA_NT_STAMP(ts1);
       __builtin_amdgcn_s_barrier();  // every wave holds chunk t: buffer b is free
+      PRA_NT_STAMP(ts2);
       __builtin_amdgcn_sched_barrier(0);
-      // phase 2: MFMA 32..111 with the 16 DMA instructions of chunk t + 2 into buffer b
+      // phase 2: MFMA P1..127-P3 with the 16 DMA instructions of chunk t + 2 into buffer b
 #pragma unroll
       for (int d = 0; d < 16; ++d) {
-        dma(b, t + 2, d);
+        if constexpr (PRA_NT_M0SPLIT) {
+          m0_set(dma_lds(b, d));
+          __builtin_amdgcn_sched_barrier(0);
+          mf(P1 + MD * d);
+          __builtin_amdgcn_sched_barrier(0);
+          dma_go(t + 2, d);
 #pragma unroll
-        for (int q = 32 + 5 * d; q < 37 + 5 * d; ++q) mf(q);
+          for (int k = 1; k < MD; ++k) mf(P1 + MD * d + k);
+        } else {
+          dma(b, t + 2, d);
+#pragma unroll
+          for (int k = 0; k < MD; ++k) mf(P1 + MD * d + k);
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
+      PRA_NT_STAMP(ts3);
       wait_vm<16>();  // chunk t + 1 landed (chunk t + 2's 16 instructions stay in flight)
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+      PRA_NT_STAMP(ts4);
+#ifdef PRA_NT_STAMPS
+      sw1 += ts2 - ts1; sp2 += ts3 - ts2; sw2 += ts4 - ts3;
+      if (ts4p) sp31 += ts1 - ts4p;
+      ts4p = ts4; ++nch;
+#endif
       __builtin_amdgcn_sched_barrier(0);
-      // phase 3: MFMA 112..127; k-substep-0 fragments of chunk t + 1 (buffer b ^ 1), first-use order
+      // phase 3: MFMA 128-P3..127 (k-substep 1: fa0 / fb0 are free); k-substep-0 fragments of
+      // chunk t + 1 (buffer b ^ 1) in first-use order
 #pragma unroll
-      for (int q = 112; q < 128; ++q) {
-        mf(q);
-        const int r = q - 112;
+      for (int r = 0; r < 16; ++r) {
+#pragma unroll
+        for (int k = 0; k < RS3; ++k) mf(128 - P3 + r * RS3 + k);
         if (r == 0)
           fa0[0] = fragA(b ^ 1, 0, 0);
         else if (r < 9)
           fb0[r - 1] = fragB(b ^ 1, 0, r - 1);
         else
           fa0[r - 8] = fragA(b ^ 1, 0, r - 8);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, RS3, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
+#pragma unroll
+      for (int q = 128 - P3 + 16 * RS3; q < 128; ++q) mf(q);
+      if constexpr (P3 > 16 * RS3) __builtin_amdgcn_sched_group_barrier(0x008, P3 - 16 * RS3, 0);
       __builtin_amdgcn_sched_barrier(0);
     };
     // four chunks per iteration with compile-time buffers (a 2-chunk body with a conditional
@@ -337,6 +419,12 @@ __global__ __launch_bounds__(NTH) void gemm_nt_kernel(const T* __restrict__ A, c
     // tail's flag overwrites
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+#ifdef PRA_NT_STAMPS
+    if (lane == 0 && pra_nt_stamp_out) {
+      unsigned long long* o = pra_nt_stamp_out + ((long)blockIdx.x * 4 + wid) * 8;
+      o[0] = sw1; o[1] = sp2; o[2] = sw2; o[3] = sp31; o[4] = nch; o[5] = ts4p;
+    }
+#endif
   };
 
   auto run = [&](long m0, long n0, int k0, int k1) __attribute__((always_inline)) {

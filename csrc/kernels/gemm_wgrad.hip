@@ -68,6 +68,10 @@ __device__ __forceinline__ i16x4 tr4(const T* tile, int byte_off) {
 // workgroup.
 // EXP (timing experiments only, tools/gemm_exp.py; results are garbage): bit 0 = no main-loop
 // LDS-DMA (prologue stages only), bit 1 = no main-loop fragment reads (stale registers)
+#ifndef PRA_WG_M0SPLIT
+#define PRA_WG_M0SPLIT 0
+#endif
+
 template <typename T, bool ACC, int EXP = 0>
 __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, const T* __restrict__ B,
                                                       T* __restrict__ C, int M, int N, int K, long lda, long ldb,
@@ -130,11 +134,16 @@ __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, c
     const T* Ab = A + m0;
     const T* Bb = B + n0;
     // DMA instruction u (0..2NI-1) of stage kt into slot s: SGPR base + per-lane byte offset
-    auto dma = [&](int s, int kt, int u) __attribute__((always_inline)) {
-      const int i = u >> 1;
-      const uint32_t lds = ldsw + (uint32_t)((s * 2 * TILE + (u & 1) * TILE) * sizeof(T) + i * 4 * 1024);
+    auto dma_lds = [&](int s, int u) __attribute__((always_inline)) {
+      return ldsw + (uint32_t)((s * 2 * TILE + (u & 1) * TILE) * sizeof(T) + (u >> 1) * 4 * 1024);
+    };
+    auto dma_go = [&](int kt, int u) __attribute__((always_inline)) {
       const T* g = (u & 1) ? Bb + (long)kt * BK * ldb : Ab + (long)kt * BK * lda;
-      dma16s(g, (u & 1) ? offb[i] : offa[i], lds);
+      dma16s_go(g, (u & 1) ? offb[u >> 1] : offa[u >> 1]);
+    };
+    auto dma = [&](int s, int kt, int u) __attribute__((always_inline)) {
+      const T* g = (u & 1) ? Bb + (long)kt * BK * ldb : Ab + (long)kt * BK * lda;
+      dma16s(g, (u & 1) ? offb[u >> 1] : offa[u >> 1], dma_lds(s, u));
     };
     // every step issues exactly one stage of DMA (a stage past k1 re-loads stage k1 - 1 into the
     // slot nobody reads again), so the counted waits are the same on every step
@@ -166,6 +175,12 @@ __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, c
       const int kd = min(kt + NS - 1, k1 - 1);
 #pragma unroll
       for (int gi = 0; gi < 8; ++gi) {
+        // PRA_WG_M0SPLIT: the group's M0 write goes first and its DMA last, so the group's MFMAs
+        // are the wait state (no s_nop)
+        if constexpr (PRA_WG_M0SPLIT && !(EXP & 1)) {
+          m0_set(dma_lds(sd, gi));
+          __builtin_amdgcn_sched_barrier(0);
+        }
         if constexpr (!(EXP & 2)) {
           na[gi] = fragA(nta, gi);
           nb[gi] = fragB(nta + TILE, gi);
@@ -181,7 +196,10 @@ __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, c
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         }
-        if constexpr (!(EXP & 1)) dma(sd, kd, gi);
+        if constexpr (PRA_WG_M0SPLIT && !(EXP & 1))
+          dma_go(kd, gi);
+        else if constexpr (!(EXP & 1))
+          dma(sd, kd, gi);
       }
     };
     // unrolled by lcm(NS, 2) = 10: compile-time ring slot and fragment register set

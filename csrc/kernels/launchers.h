@@ -82,7 +82,9 @@ hipError_t pra_attn_bwd(int dtype, const void* q, const void* k, const void* v, 
                         int D, long ldq, long ldk, long ldv, long ldo, long lddo, long lddq, long lddk, long lddv,
                         float scale, int causal, int skv, const float* rope_tab, hipEvent_t mid_event,
                         hipStream_t st);
-void pra_attn_set_options(int fwd_pipe, float fwd_thr, int dkdv_impl, int dq_pipe);
+void pra_attn_set_options(int fwd_pipe, float fwd_thr, int dkdv_impl, int dq_pipe, int dkdv_split, int dkdv_kreg);
+// floats of fp32 workspace pra_attn_bwd needs at `delta` (delta, row constants, split dK/dV parts)
+long pra_attn_bwd_workspace(int dtype, int B, int S, int Hq, int Hkv, int D);
 // fp32 flash attention (attention_f32.hip, f32-input MFMA); pra_attn_fwd / pra_attn_bwd route kF32 here
 hipError_t pra_attn_fwd_f32(const float* q, const float* k, const float* v, float* o, float* lse, int B, int S, int Hq,
                             int Hkv, int D, long ldq, long ldk, long ldv, long ldo, float scale, int causal, int skv,

@@ -92,7 +92,7 @@ def test_untiled_seq_len(cuda, S, causal, dtype):
 
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(1, 2048, 32, 32), (1, 8192, 32, 8)])
 def test_production_shapes_default_kernels(cuda, attn_opts, B, S, Hq, Hkv):
-    attn_opts(fwd_pipe=None, fwd_thr=None, dkdv_impl=None, dq_pipe=None)
+    attn_opts(fwd_pipe=None, fwd_thr=None, dkdv_impl=None, dq_pipe=None, dkdv_split=None, dkdv_kreg=None)
     q, k, v, o, lse, do, dq, dk, dv = _run(cuda, B, S, Hq, Hkv, 128, True, torch.bfloat16, seed=7)
     # bit-reproducible backward at production shape (bit-exact resume relies on it)
     dq2, dk2, dv2 = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)

@@ -255,14 +255,15 @@ def test_attention_bwd(cuda, B, S, Hq, Hkv, D, causal):
     assert torch.equal(dqkv, dqkv2)
 
 
-@pytest.mark.parametrize("impl", [0, 1])
+@pytest.mark.parametrize("impl", [0, 1, 2])
 @pytest.mark.parametrize("B,S,Hq,Hkv,D,causal", [(1, 1024, 4, 1, 128, True), (2, 512, 4, 2, 128, False),
                                                  (1, 640, 2, 2, 64, True)])
 def test_attention_bwd_dkdv_kernels(cuda, attn_opts, impl, B, S, Hq, Hkv, D, causal):
     """Both backward kernel generations -- dK/dV two-wave vs one-wave-per-SIMD pipelined
     (dkdv_impl), dQ plain vs region-pipelined (dq_pipe) -- against the fp32 oracle, with
-    multi-step loops, GQA and the causal diagonal."""
-    attn_opts(dkdv_impl=impl, dq_pipe=impl)
+    multi-step loops, GQA and the causal diagonal. impl 2: the two-wave kernel with K held in
+    registers (dkdv_kreg; 256-key blocks at D = 128)."""
+    attn_opts(dkdv_impl=min(impl, 1) if impl < 2 else 0, dq_pipe=min(impl, 1), dkdv_kreg=int(impl == 2))
     C = _ext.native()
     _, q, k, v = _qkv(cuda, B, S, Hq, Hkv, D, seed=5)
     scale = 1 / math.sqrt(D)
@@ -278,6 +279,45 @@ def test_attention_bwd_dkdv_kernels(cuda, attn_opts, impl, B, S, Hq, Hkv, D, cau
     dq2, dk2, dv2 = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
     C.attn_bwd(q, k, v, o, do, lse, dq2, dk2, dv2, scale, causal)
     assert torch.equal(dq, dq2) and torch.equal(dk, dk2) and torch.equal(dv, dv2)
+
+
+@pytest.mark.parametrize("split", [2, 4])
+@pytest.mark.parametrize("B,S,Hq,Hkv,D,causal,rope", [(1, 1024, 8, 2, 128, True, True), (2, 512, 4, 1, 128, False, False),
+                                                      (1, 640, 4, 1, 64, True, True)])
+def test_attention_bwd_dkdv_query_head_split(cuda, attn_opts, split, B, S, Hq, Hkv, D, causal, rope):
+    """The pipelined dK/dV kernel with the kv head's query heads split over blocks (fp32 parts plus the
+    reduction pass, the small-batch GQA path): against the fp32 oracle and the unsplit kernel, with the
+    fused inverse RoPE on dK, and deterministic run to run."""
+    from pyrecover_amd.ops.reference import precompute_freqs_cis, rope_table
+
+    C = _ext.native()
+    _, q, k, v = _qkv(cuda, B, S, Hq, Hkv, D, seed=11)
+    scale = 1 / math.sqrt(D)
+    tab = rope_table(precompute_freqs_cis(D, S, 10000.0)).to(cuda) if rope else None
+    o, lse = C.attn_fwd(q, k, v, scale, causal)
+    do = torch.randn(B, S, Hq, D, device=cuda).bfloat16()
+    res = {}
+    for n in (1, split, split):
+        attn_opts(dkdv_impl=1, dkdv_split=n)
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        C.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, causal, tab)
+        if n in res:
+            assert all(torch.equal(a, b) for a, b in zip(res[n], (dq, dk, dv)))
+        res[n] = (dq, dk, dv)
+    qf, kf, vf = (t.float().requires_grad_() for t in (q, k, v))
+    of, _ = R.attention_lse_ref(qf, kf, vf, causal, scale)
+    of.backward(do.float())
+    dk32 = kf.grad
+    if rope:
+        dk32 = dk32.reshape(B * S, Hkv * D).clone()
+        R.rope_inplace_2d(dk32, Hkv * D, tab, D, S, inverse=True)
+        dk32 = dk32.view(B, S, Hkv, D)
+    dq, dk, dv = res[split]
+    assert torch.equal(dq, res[1][0])  # the dQ kernel is not split
+    for got, want in ((dk, dk32), (dv, vf.grad)):
+        assert _rel(got, want) < 3e-2, _rel(got, want)
+    for got, base in ((dk, res[1][1]), (dv, res[1][2])):
+        assert _rel(got, base.float()) < 1e-2
 
 
 @pytest.mark.parametrize("impl", [0, 1])

@@ -19,7 +19,7 @@ import torch  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--opt", required=True, choices=["fwd_pipe", "fwd_thr", "dkdv_impl", "dq_pipe"])
+    ap.add_argument("--opt", required=True, choices=["fwd_pipe", "fwd_thr", "dkdv_impl", "dq_pipe", "dkdv_split", "dkdv_kreg"])
     ap.add_argument("--values", default="0,1")
     ap.add_argument("--B", type=int, default=16)
     ap.add_argument("--S", type=int, default=2048)
