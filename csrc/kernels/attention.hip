@@ -1323,9 +1323,10 @@ struct AttnOptions {
   // pipelined dK/dV kernel, query heads per block: -1 = by grid size (dkdv_split), 1 = all of the
   // kv head's Hq / Hkv heads in one block, n = Hq / Hkv / n heads per block plus an fp32 reduction
   int dkdv_split = -1;
-  // two-wave dK/dV kernel (NW = 8, D = 128): 1 = K fragments held in registers (KREG), 0 = read from LDS
+  // two-wave dK/dV kernel (NW = 8, D = 128): 1 = K fragments held in registers (KREG), 0 = read from
+  // LDS, -1 = KREG unless a side-stream job waits for the dK/dV window (below)
   // (B16 S2048 H32 bwd 2.387 -> 2.358 ms: profiles/r4/attn_ab_dkdv_kreg_b16.log)
-  int dkdv_kreg = 1;
+  int dkdv_kreg = -1;
 };
 AttnOptions g_attn_opts;
 
@@ -1367,6 +1368,13 @@ static bool dkdv_use_p2(int B, int S, int Hq, int Hkv, int D) {
   return impl == 1 || (impl < 0 && (D == 64 || ((long)(Hq / Hkv) * S >= 8192 && grid2 <= 256)));
 }
 
+// Window rule (dkdv_split / dkdv_kreg = -1): when the caller hands a mid_event, a side-stream job
+// (the overlapped AdamW update, ops/sched.py) runs beside the dK/dV kernel, and a shorter kernel only
+// pushes the rest of that job onto the GEMMs after it. In the step, the faster variants then lose:
+// Llama-3-8B B1 S2048 109.1 ms split vs 108.3 unsplit (eager update: 109.7 vs 113.6), 7B B16
+// 1058.0 KREG vs 1055.5 (profiles/r4/step_ab_*_split_sched.log, *_kreg.log). So both apply only
+// when no job waits for the window (e.g. gradient-accumulation micro-steps, no overlapped update).
+//
 // GQA at small batch: the pipelined dK/dV grid is (S / 128) Hkv B blocks, one per CU at D = 128
 // (Llama-3-8B B1 S2048 bwd 0.297 -> 0.206 (2 splits) -> 0.172 ms (4); S8192: 1.717 ms unsplit, the
 // best: profiles/r4/attn_ab_dkdv_split_*.log)
@@ -1437,8 +1445,9 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
 #undef LAUNCH
   }
   if (mid_event != nullptr) hipEventRecord(mid_event, st);  // between the dQ and dK/dV launches
+  const bool window = mid_event != nullptr;
   if (p2) {
-    const int ns = dkdv_split(B, S, Hq, Hkv, D);
+    const int ns = window && g_attn_opts.dkdv_split < 0 ? 1 : dkdv_split(B, S, Hq, Hkv, D);
     float* part = ns > 1 ? delta + 3 * nrc : nullptr;  // attn_bwd_ws_floats
     dim3 g1((S / 128) * Hkv * B * ns);
 #define LAUNCH1(DD, CC)                                                                                       \
@@ -1460,7 +1469,8 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
                      (const T*)k,                                                                               \
                      (const T*)v, (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Hq, Hkv, ldq, ldk, ldv, lddo,  \
                      lddk, lddv, scale, sl2, skv, rt)
-    if (nw == 8 && D == 128 && g_attn_opts.dkdv_kreg == 1) {
+    const bool kreg = g_attn_opts.dkdv_kreg == 1 || (g_attn_opts.dkdv_kreg < 0 && !window);
+    if (nw == 8 && D == 128 && kreg) {
       if (causal) LAUNCH(128, true, 8, true); else LAUNCH(128, false, 8, true);
     } else if (nw == 8) {
       if (D == 128) { if (causal) LAUNCH(128, true, 8); else LAUNCH(128, false, 8); }

@@ -68,8 +68,11 @@ __device__ __forceinline__ i16x4 tr4(const T* tile, int byte_off) {
 // workgroup.
 // EXP (timing experiments only, tools/gemm_exp.py; results are garbage): bit 0 = no main-loop
 // LDS-DMA (prologue stages only), bit 1 = no main-loop fragment reads (stale registers)
+// 1: each DMA group's M0 write first, its load last (no s_nop): 4096x4096x32768 1481-1509 -> 1514-1538
+// TF, 11008x4096x32768 1366-1376 -> 1407-1410 TF (tools/wgrad_variants.hip,
+// profiles/r4/wgrad_m0split_ab.log)
 #ifndef PRA_WG_M0SPLIT
-#define PRA_WG_M0SPLIT 0
+#define PRA_WG_M0SPLIT 1
 #endif
 
 template <typename T, bool ACC, int EXP = 0>

@@ -312,6 +312,21 @@ def test_attention_bwd_dkdv_query_head_split(cuda, attn_opts, split, B, S, Hq, H
         dk32 = dk32.reshape(B * S, Hkv * D).clone()
         R.rope_inplace_2d(dk32, Hkv * D, tab, D, S, inverse=True)
         dk32 = dk32.view(B, S, Hkv, D)
+    # by-grid default (-1): split without a window job, unsplit when a side-stream job waits for the
+    # dK/dV window (mid_event)
+    attn_opts(dkdv_impl=1, dkdv_split=None)
+    for with_event in (False, True):
+        ev = torch.cuda.Event()
+        ev.record()
+        d3 = [torch.empty_like(t) for t in (q, k, v)]
+        C.attn_bwd(q, k, v, o, do, lse, *d3, scale, causal, tab, ev.cuda_event if with_event else 0)
+        torch.cuda.synchronize()
+        n, grid = 1, (S // 128) * Hkv * B  # attention.hip dkdv_split(): the by-grid choice
+        while grid * n < (512 if D == 128 else 1024) and (Hq // Hkv) % (2 * n) == 0:
+            n *= 2
+        want = res[1] if with_event else res.get(n)
+        if want is not None:
+            assert all(torch.equal(a, b) for a, b in zip(d3, want)), with_event
     dq, dk, dv = res[split]
     assert torch.equal(dq, res[1][0])  # the dQ kernel is not split
     for got, want in ((dk, dk32), (dv, vf.grad)):
