@@ -71,9 +71,6 @@ __device__ __forceinline__ i16x4 tr4(const T* tile, int byte_off) {
 // 1: each DMA group's M0 write first, its load last (no s_nop): 4096x4096x32768 1481-1509 -> 1514-1538
 // TF, 11008x4096x32768 1366-1376 -> 1407-1410 TF (tools/wgrad_variants.hip,
 // profiles/r4/wgrad_m0split_ab.log)
-#ifndef PRA_WG_INCPTR
-#define PRA_WG_INCPTR 0
-#endif
 #ifndef PRA_WG_M0SPLIT
 #define PRA_WG_M0SPLIT 1
 #endif
@@ -143,13 +140,10 @@ __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, c
     auto dma_lds = [&](int s, int u) __attribute__((always_inline)) {
       return ldsw + (uint32_t)((s * 2 * TILE + (u & 1) * TILE) * sizeof(T) + (u >> 1) * 4 * 1024);
     };
-    // PRA_WG_INCPTR: the stage base pointers of the main loop's DMAs advance by one stage per step
-    // (two 64-bit SGPR adds) instead of being recomputed from the stage index per DMA
-    const T* dga = Ab + (long)min(k0 + NS - 1, k1 - 1) * BK * lda;
-    const T* dgb = Bb + (long)min(k0 + NS - 1, k1 - 1) * BK * ldb;
+    // (advancing the stage base pointers by one stage per step instead of recomputing them per DMA
+    // cut the loop's SALU from ~40 to ~15 per stage and measured equal: profiles/r4/wgrad_incptr_ab.log)
     auto dma_go = [&](int kt, int u) __attribute__((always_inline)) {
-      const T* g = PRA_WG_INCPTR ? ((u & 1) ? dgb : dga)
-                                 : ((u & 1) ? Bb + (long)kt * BK * ldb : Ab + (long)kt * BK * lda);
+      const T* g = (u & 1) ? Bb + (long)kt * BK * ldb : Ab + (long)kt * BK * lda;
       dma16s_go(g, (u & 1) ? offb[u >> 1] : offa[u >> 1]);
     };
     auto dma = [&](int s, int kt, int u) __attribute__((always_inline)) {
@@ -212,12 +206,7 @@ __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, c
         else if constexpr (!(EXP & 1))
           dma(sd, kd, gi);
       }
-      if constexpr (PRA_WG_INCPTR) {
-        if (kt + NS < k1) {  // past the end the last stage is re-loaded (see the prologue)
-          dga += BK * lda;
-          dgb += BK * ldb;
-        }
-      }
+
     };
     // unrolled by lcm(NS, 2) = 10: compile-time ring slot and fragment register set
     constexpr int UNR = 10;
