@@ -24,6 +24,16 @@ using V8 = typename Elem<T>::v8;
 template <int N>
 using IC = std::integral_constant<int, N>;
 
+// f(IC<I>{}) for I in [I0, N): a compile-time loop (a 128-step #pragma unroll body with nested loops
+// can stay rolled, which turns register arrays into scratch)
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
 constexpr int BM = 256, BN = 256, BK = 32, NTH = 256, NS = 5;
 constexpr int TILE = BK * 256;              // elements per staged operand tile (16 KiB)
 constexpr int NI = TILE * 2 / (NTH * 16);   // LDS-DMA instructions per lane per operand tile (4)
@@ -53,8 +63,10 @@ __device__ __forceinline__ void dma16s_go(const void* sbase, uint32_t voff) {
 // s_waitcnt vmcnt(N) for a compile-time N
 template <int N>
 __device__ __forceinline__ void wait_vm() {
-  static_assert(N == 0 || N == 8 || N == 16 || N == 24 || N == 32, "add the count");
+  static_assert(N == 0 || N == 8 || N == 15 || N == 16 || N == 18 || N == 24 || N == 32, "add the count");
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (N == 15) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+  if constexpr (N == 18) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
   if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");

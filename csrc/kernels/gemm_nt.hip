@@ -83,6 +83,16 @@ __device__ unsigned long long* pra_nt_stamp_out;
   } while (0)
 #endif
 
+// SCHED 1 (hipBLASLt's chunk order, 4 barriers) vs 0 (3 phases, 2 barriers) and VOFF (per-DMA row
+// offsets in VGPRs) at 32768x4096x4096, three interleaved rounds: 3-phase 1438, 4-barrier 1445,
+// 4-barrier + VOFF 1449, 3-phase + VOFF 1454 TF (the VGPR offsets take ~50 cycles per chunk off
+// phase 2); hipBLASLt 1508-1580 on this shape (profiles/r4/gemm_nt_hipblaslt_order*.log)
+#ifndef PRA_NT_SCHED
+#define PRA_NT_SCHED 0
+#endif
+#ifndef PRA_NT_VOFF
+#define PRA_NT_VOFF 1
+#endif
 #ifndef PRA_NT_P1
 #define PRA_NT_P1 32
 #endif
@@ -101,6 +111,23 @@ __device__ unsigned long long* pra_nt_stamp_out;
 #ifndef PRA_NT_M0SPLIT
 #define PRA_NT_M0SPLIT 1
 #endif
+
+// PRA_NT_SCHED 1 event tables: the MFMA index after which DMA d (A rows 0..7, B rows 8..15) of
+// chunk t + 2 issues, and after which fragment read 8 g + r issues (g: 0 fb1, 1 fa1 of chunk t;
+// 2 fb0, 3 fa0 of chunk t + 1)
+constexpr int kNt4Dma[16] = {61, 64, 85, 87, 89, 94, 98, 124, 22, 25, 28, 31, 34, 52, 55, 58};
+constexpr int kNt4Read[32] = {1,   3,   5,   7,   9,   11,  13,  15,  24, 27, 30, 33, 36, 38, 40, 42,
+                              69,  71,  73,  75,  77,  79,  81,  83,  106, 108, 110, 112, 114, 116, 118, 120};
+constexpr int nt4_dma_at(int q) {
+  for (int d = 0; d < 16; ++d)
+    if (kNt4Dma[d] == q) return d;
+  return -1;
+}
+constexpr int nt4_read_at(int q) {
+  for (int i = 0; i < 32; ++i)
+    if (kNt4Read[i] == q) return i;
+  return -1;
+}
 
 // the XOR swizzle of the 16-B chunk of row r: g((r >> 2) & 3), g = {0, 2, 3, 1}
 __device__ __forceinline__ int swz(int r) {
@@ -293,10 +320,12 @@ __global__ __launch_bounds__(NTH) void gemm_nt_kernel(const T* __restrict__ A, c
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // B rows first (d = 8..15, then 0..7): the 4-barrier schedule waits for a chunk's B half
+    // before its A half
 #pragma unroll
-    for (int d = 0; d < 16; ++d) dma(0, c0, d);
+    for (int e = 0; e < 16; ++e) dma(0, c0, (e + 8) & 15);
 #pragma unroll
-    for (int d = 0; d < 16; ++d) dma(1, c0 + 1, d);
+    for (int e = 0; e < 16; ++e) dma(1, c0 + 1, (e + 8) & 15);
     wait_vm<16>();  // chunk c0 landed; c0 + 1 stays in flight
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -326,10 +355,21 @@ __global__ __launch_bounds__(NTH) void gemm_nt_kernel(const T* __restrict__ A, c
     auto dma_lds = [&](int b, int d) __attribute__((always_inline)) {
       return ldsw + (uint32_t)((b * 2 + (d >> 3)) * TILE64 * sizeof(T) + (d & 7) * 4 * 1024);
     };
+    // PRA_NT_VOFF: each DMA's row offset lives in a VGPR (16 loop-invariant registers), so the SGPR
+    // base only moves once per chunk and operand instead of once per DMA (hipBLASLt's form)
+    uint32_t vo[PRA_NT_VOFF ? 16 : 1];
+    if constexpr (PRA_NT_VOFF) {
+#pragma unroll
+      for (int d = 0; d < 16; ++d)
+        vo[d] = d >= 8 ? vob64 + (uint32_t)((long)row_b64(d & 7) * ldb * (long)sizeof(T))
+                       : voa64 + (uint32_t)((long)row_a64(d & 7) * lda * (long)sizeof(T));
+    }
     auto dma_go = [&](int c, int d) __attribute__((always_inline)) {
       c = min(c, c1 - 1);
       const int i = d & 7;
-      if (d >= 8)
+      if constexpr (PRA_NT_VOFF)
+        dma16s_go((d >= 8 ? Bb : Ab) + (long)c * 64, vo[PRA_NT_VOFF ? d : 0]);
+      else if (d >= 8)
         dma16s_go(Bb + (long)row_b64(i) * ldb + (long)c * 64, vob64);
       else
         dma16s_go(Ab + (long)row_a64(i) * lda + (long)c * 64, voa64);
@@ -407,13 +447,71 @@ __global__ __launch_bounds__(NTH) void gemm_nt_kernel(const T* __restrict__ A, c
       if constexpr (P3 > 16 * RS3) __builtin_amdgcn_sched_group_barrier(0x008, P3 - 16 * RS3, 0);
       __builtin_amdgcn_sched_barrier(0);
     };
+    // PRA_NT_SCHED 1: hipBLASLt's 256x256x64 DTL/PGR2 chunk order (read off its gfx950 ISA), four
+    // barriers per chunk so every phase frees or publishes one operand half:
+    //   MFMA 0-19    B k-substep-1 reads of chunk t (1 per 2 MFMA); lgkmcnt(0) + barrier 1: B half free
+    //   MFMA 20-50   5 B DMAs of chunk t + 2, A k-substep-1 reads; lgkmcnt(0) + barrier 2: A half free
+    //   MFMA 51-67   3 B + 2 A DMAs; vmcnt(18) + barrier 3: chunk t + 1's B half landed
+    //   MFMA 68-104  B k-substep-0 reads of chunk t + 1 (fb0 is free after MFMA 63), 5 A DMAs;
+    //                vmcnt(15) + barrier 4: chunk t + 1 landed
+    //   MFMA 105-127 A k-substep-0 reads of chunk t + 1, the last A DMA
+    // Every DMA's M0 write sits one MFMA ahead of its load.
+    auto chunk4 = [&](auto b_c, int t) __attribute__((always_inline)) {
+      constexpr int b = decltype(b_c)::value;
+      __builtin_amdgcn_sched_barrier(0);
+      static_for<0, 128>([&](auto q_c) __attribute__((always_inline)) {
+        constexpr int q = decltype(q_c)::value;
+        mf(q);
+        constexpr int rd = nt4_read_at(q), dd = nt4_dma_at(q), md = nt4_dma_at(q + 1);
+        if constexpr (rd >= 0) {
+          constexpr int g = rd >> 3, r = rd & 7;
+          if constexpr (g == 0) fb1[r] = fragB(b, 1, r);
+          if constexpr (g == 1) fa1[r] = fragA(b, 1, r);
+          if constexpr (g == 2) fb0[r] = fragB(b ^ 1, 0, r);
+          if constexpr (g == 3) fa0[r] = fragA(b ^ 1, 0, r);
+        }
+        if constexpr (dd >= 0) dma_go(t + 2, dd);
+        if constexpr (md >= 0) m0_set(dma_lds(b, md));  // one MFMA ahead of its load
+        if constexpr (q == 19 || q == 50) {
+          __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+          if constexpr (q == 19) PRA_NT_STAMP(ts1);
+          __builtin_amdgcn_s_barrier();
+          if constexpr (q == 19) PRA_NT_STAMP(ts2);
+        }
+        if constexpr (q == 67) {
+          PRA_NT_STAMP(ts3);
+          wait_vm<18>();
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+          PRA_NT_STAMP(ts4);
+        }
+        if constexpr (q == 104) {
+          wait_vm<15>();
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+#ifdef PRA_NT_STAMPS
+      sw1 += ts2 - ts1; sp2 += ts3 - ts2; sw2 += ts4 - ts3;
+      if (ts4p) sp31 += ts1 - ts4p;
+      ts4p = ts4; ++nch;
+#endif
+    };
     // four chunks per iteration with compile-time buffers (a 2-chunk body with a conditional
     // second chunk broke the accumulator register coalescing: 100+ spills)
     for (int t = c0; t < c1; t += 4) {
-      if (t < c1) chunk(IC<0>{}, t);
-      if (t + 1 < c1) chunk(IC<1>{}, t + 1);
-      if (t + 2 < c1) chunk(IC<0>{}, t + 2);
-      if (t + 3 < c1) chunk(IC<1>{}, t + 3);
+      if constexpr (PRA_NT_SCHED == 1) {
+        if (t < c1) chunk4(IC<0>{}, t);
+        if (t + 1 < c1) chunk4(IC<1>{}, t + 1);
+        if (t + 2 < c1) chunk4(IC<0>{}, t + 2);
+        if (t + 3 < c1) chunk4(IC<1>{}, t + 3);
+      } else {
+        if (t < c1) chunk(IC<0>{}, t);
+        if (t + 1 < c1) chunk(IC<1>{}, t + 1);
+        if (t + 2 < c1) chunk(IC<0>{}, t + 2);
+        if (t + 3 < c1) chunk(IC<1>{}, t + 3);
+      }
     }
     // no LDS-DMA may land after this point, and no wave may still read a buffer the split
     // tail's flag overwrites
