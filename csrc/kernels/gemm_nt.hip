@@ -90,6 +90,12 @@ __device__ unsigned long long* pra_nt_stamp_out;
 #ifndef PRA_NT_SCHED
 #define PRA_NT_SCHED 0
 #endif
+// ST16: epilogue stores of 16 B (v_permlane16_swap pairs two 16-column blocks) instead of 8 B: per
+// 256x256 tile 11.8k instead of 16.1k cycles from loop end to stores retired; 32768x11008x4096
+// 1434 -> 1466 TF (profiles/r4/gemm_nt_st16_epilogue.log)
+#ifndef PRA_NT_ST16
+#define PRA_NT_ST16 1
+#endif
 #ifndef PRA_NT_VOFF
 #define PRA_NT_VOFF 1
 #endif
@@ -217,9 +223,9 @@ __global__ __launch_bounds__(NTH) void gemm_nt_kernel(const T* __restrict__ A, c
         T* rowp = C + row * ldc + n0 + 128 * wn + 4 * g4;
         int pos = 0;
         if constexpr (EPI == 3) pos = (int)(row % ep.S);
+        auto vals = [&](int j, float (&v)[4]) __attribute__((always_inline)) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e];
           if constexpr (EPI == 3) {
             const int col = (int)n0 + 128 * wn + 16 * j + 4 * g4;
             if (col < ep.nrot) {
@@ -229,7 +235,28 @@ __global__ __launch_bounds__(NTH) void gemm_nt_kernel(const T* __restrict__ A, c
               rot_pair(a1, b1, cs.z, cs.w, v[2], v[3]);
             }
           }
-          *reinterpret_cast<uint2*>(rowp + 16 * j) = make_uint2(pack_x2<T>(v[0], v[1]), pack_x2<T>(v[2], v[3]));
+        };
+        if constexpr (PRA_NT_ST16) {
+          // blocks j, j + 1 through v_permlane16_swap (lane rows g4 even <-> odd): lane row g4
+          // ends up with 8 consecutive columns, 16 (j + (g4 & 1)) + 8 (g4 >> 1) + 0..7, and stores
+          // them as one 16-B write (32 instead of 64 store instructions per lane)
+          T* sp = C + row * ldc + n0 + 128 * wn + 16 * (g4 & 1) + 8 * (g4 >> 1);
+#pragma unroll
+          for (int j = 0; j < 8; j += 2) {
+            float va[4], vb[4];
+            vals(j, va);
+            vals(j + 1, vb);
+            const auto s0 = __builtin_amdgcn_permlane16_swap(pack_x2<T>(va[0], va[1]), pack_x2<T>(vb[0], vb[1]), false, false);
+            const auto s1 = __builtin_amdgcn_permlane16_swap(pack_x2<T>(va[2], va[3]), pack_x2<T>(vb[2], vb[3]), false, false);
+            *reinterpret_cast<uint4*>(sp + 16 * j) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float v[4];
+            vals(j, v);
+            *reinterpret_cast<uint2*>(rowp + 16 * j) = make_uint2(pack_x2<T>(v[0], v[1]), pack_x2<T>(v[2], v[3]));
+          }
         }
       } else if constexpr (EPI == 1) {
         // features f0 + 16 j + 4 g4 + 0..3 (j < 4): gate in acc[i][j], up in acc[i][j + 4]
@@ -237,8 +264,7 @@ __global__ __launch_bounds__(NTH) void gemm_nt_kernel(const T* __restrict__ A, c
         T* gp = C + row * ldc + f0;
         T* up = gp + ep.F;
         T* ap = ep.c2 + row * ep.ldc2 + f0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        auto gua = [&](int j, uint32_t (&o)[6]) __attribute__((always_inline)) {  // g, u, a packed pairs
           float g[4], u[4], a[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -246,9 +272,34 @@ __global__ __launch_bounds__(NTH) void gemm_nt_kernel(const T* __restrict__ A, c
             u[e] = rnd16<T>(acc[i][j + 4][e]);
             a[e] = rnd16<T>(silu_f(g[e])) * u[e];
           }
-          *reinterpret_cast<uint2*>(gp + 16 * j) = make_uint2(pack_x2<T>(g[0], g[1]), pack_x2<T>(g[2], g[3]));
-          *reinterpret_cast<uint2*>(up + 16 * j) = make_uint2(pack_x2<T>(u[0], u[1]), pack_x2<T>(u[2], u[3]));
-          *reinterpret_cast<uint2*>(ap + 16 * j) = make_uint2(pack_x2<T>(a[0], a[1]), pack_x2<T>(a[2], a[3]));
+          o[0] = pack_x2<T>(g[0], g[1]); o[1] = pack_x2<T>(g[2], g[3]);
+          o[2] = pack_x2<T>(u[0], u[1]); o[3] = pack_x2<T>(u[2], u[3]);
+          o[4] = pack_x2<T>(a[0], a[1]); o[5] = pack_x2<T>(a[2], a[3]);
+        };
+        if constexpr (PRA_NT_ST16) {  // as EPI 0: features 16 (j + (g4 & 1)) + 8 (g4 >> 1) + 0..7 per lane
+          const long s0 = (16 * (g4 & 1) + 8 * (g4 >> 1)) - 4 * g4;
+#pragma unroll
+          for (int j = 0; j < 4; j += 2) {
+            uint32_t x[6], y[6];
+            gua(j, x);
+            gua(j + 1, y);
+            T* dst[3] = {gp + s0 + 16 * j, up + s0 + 16 * j, ap + s0 + 16 * j};
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+              const auto w0 = __builtin_amdgcn_permlane16_swap(x[2 * k], y[2 * k], false, false);
+              const auto w1 = __builtin_amdgcn_permlane16_swap(x[2 * k + 1], y[2 * k + 1], false, false);
+              *reinterpret_cast<uint4*>(dst[k]) = make_uint4(w0[0], w1[0], w0[1], w1[1]);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            uint32_t x[6];
+            gua(j, x);
+            *reinterpret_cast<uint2*>(gp + 16 * j) = make_uint2(x[0], x[1]);
+            *reinterpret_cast<uint2*>(up + 16 * j) = make_uint2(x[2], x[3]);
+            *reinterpret_cast<uint2*>(ap + 16 * j) = make_uint2(x[4], x[5]);
+          }
         }
       } else {  // EPI == 2: dg = silu'(g) * round(da * u), du = round(da * round(silu(g))) in place over gu
         T* gp = C + row * ldc + n0 + 128 * wn + 4 * g4;
@@ -296,6 +347,10 @@ __global__ __launch_bounds__(NTH) void gemm_nt_kernel(const T* __restrict__ A, c
   // Measured and not kept (profiles/r4/): the same loop as persistent workgroups walking several
   // tiles (1-6% slower: static tile assignment loses the hardware's dynamic dispatch), on a padded
   // unswizzled LDS image (5-8% slower: 2-way bank conflicts), with buffer-form LDS-DMA (equal).
+#ifdef PRA_NT_STAMPS
+  unsigned long long ts1, ts2, ts3, ts4, ts4p = 0, sw1 = 0, sp2 = 0, sw2 = 0, sp31 = 0, nch = 0;
+  unsigned long long tk0 = 0, tk1 = 0, tk2 = 0, tk3 = 0;  // tile: start, prologue landed, loop end, stored
+#endif
   auto run2b = [&](long m0, long n0, int c0, int c1) __attribute__((always_inline)) {
     const T* Ab = A + m0 * lda;
     const T* Bb = B + (EPI == 1 ? n0 / 2 : n0) * ldb;
@@ -329,6 +384,7 @@ __global__ __launch_bounds__(NTH) void gemm_nt_kernel(const T* __restrict__ A, c
     wait_vm<16>();  // chunk c0 landed; c0 + 1 stays in flight
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    PRA_NT_STAMP(tk1);
     fa0[0] = fragA(0, 0, 0);
 #pragma unroll
     for (int f = 0; f < 8; ++f) fb0[f] = fragB(0, 0, f);
@@ -342,9 +398,6 @@ __global__ __launch_bounds__(NTH) void gemm_nt_kernel(const T* __restrict__ A, c
       else
         acc[i][j] = mfma16(fb1[j], fa1[i], acc[i][j]);
     };
-#ifdef PRA_NT_STAMPS
-    unsigned long long ts1, ts2, ts3, ts4, ts4p = 0, sw1 = 0, sp2 = 0, sw2 = 0, sp31 = 0, nch = 0;
-#endif
     // schedule knobs (defaults: the production schedule; tools/nt_stamps.hip builds variants):
     // P1 / P3 MFMAs in phases 1 / 3, one fragment read per RS1 / RS3 MFMAs, phase 2 = the rest with
     // the 16 DMAs spread evenly; M0SPLIT puts one MFMA between each DMA's M0 write and its load
@@ -517,12 +570,7 @@ __global__ __launch_bounds__(NTH) void gemm_nt_kernel(const T* __restrict__ A, c
     // tail's flag overwrites
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-#ifdef PRA_NT_STAMPS
-    if (lane == 0 && pra_nt_stamp_out) {
-      unsigned long long* o = pra_nt_stamp_out + ((long)blockIdx.x * 4 + wid) * 8;
-      o[0] = sw1; o[1] = sp2; o[2] = sw2; o[3] = sp31; o[4] = nch; o[5] = ts4p;
-    }
-#endif
+    PRA_NT_STAMP(tk2);
   };
 
   auto run = [&](long m0, long n0, int k0, int k1) __attribute__((always_inline)) {
@@ -617,6 +665,7 @@ __global__ __launch_bounds__(NTH) void gemm_nt_kernel(const T* __restrict__ A, c
   }
   long m0, n0;
   tile_origin(lin, tiles_m, tiles_n, m0, n0);
+  PRA_NT_STAMP(tk0);
   if constexpr (KB == 64)
     run2b(m0, n0, k0, k1);
   else
@@ -661,6 +710,15 @@ __global__ __launch_bounds__(NTH) void gemm_nt_kernel(const T* __restrict__ A, c
     }
   }
   store_c(m0, n0);
+#ifdef PRA_NT_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the stores have left the wave
+  PRA_NT_STAMP(tk3);
+  if (lane == 0 && pra_nt_stamp_out) {
+    unsigned long long* o = pra_nt_stamp_out + ((long)blockIdx.x * 4 + wid) * 8;
+    o[0] = sw1; o[1] = sp2; o[2] = sw2; o[3] = sp31; o[4] = nch; o[5] = tk2 - tk1; o[6] = tk1 - tk0;
+    o[7] = tk3 - tk2;
+  }
+#endif
 }
 
 __global__ __launch_bounds__(256) void zero_i32_kernel(int* __restrict__ p, int n) {

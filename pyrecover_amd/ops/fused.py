@@ -198,15 +198,21 @@ def _wgrad_into(slot, dy2, x2, shape, site, force=False):
 # both operands K-contiguous (activations [T, in] x weights [out, in]; the data gradients use the
 # transposed weight shadows), with fused epilogues where a separate memory-bound pass followed:
 # RoPE on the QKV projection, SwiGLU on the W1|W3 projection, the SwiGLU backward on the W2 data
-# gradient. With round 4's two-buffer main loop the kernel runs at 0.90-0.94 of hipBLASLt on the
-# 7B shapes (1.38-1.49 vs 1.53-1.63 PF; steady state 1.51 vs 1.65 PF, profiles/r4/), and in the
-# whole step the fused epilogues still do not win it back (7B B16: W1|W3 + SwiGLU +0.7%, W2 data
-# grad + SwiGLU backward +1.0%, both + QKV/RoPE +2.1% ms/step; profiles/r4/
-# step_ab_fused_epilogues.log), so "auto" keeps every NT site on hipBLASLt. PYRECOVER_GEMM: "auto" (default), "hip" (every valid site on the NT kernel), "lib",
+# gradient. Round 4: the NT kernel runs at 0.90-0.97 of hipBLASLt on the 7B shapes (two-buffer loop,
+# M0 writes one MFMA ahead of each LDS-DMA, row offsets in VGPRs, 16-B epilogue stores:
+# profiles/r4/gemm_nt_bench_st16.log), and the W1|W3 projection with the SwiGLU epilogue beats
+# hipBLASLt + the separate SwiGLU kernel: 4057 vs 4173 us per layer, 7B B16 step 1039.2 -> 1034.9 ms
+# (profiles/r4/step_ab_fused_swiglu_st16.log). Plain NT sites stay on hipBLASLt (adding the output
+# projection: 1037.4 ms). "auto" therefore runs w13 on the NT kernel. PYRECOVER_GEMM: "auto"
+# (default), "hip" (every valid site on the NT kernel), "lib",
 # or a comma list of sites: forward qkv, o, w13, w2, head; data gradient qkv_d, o_d, w13_d, w2_d,
 # head_d.
 _NT_ALL = frozenset({"qkv", "o", "w13", "w2", "head", "qkv_d", "o_d", "w13_d", "w2_d", "head_d"})
-_NT_AUTO = frozenset()
+_NT_AUTO = frozenset({"w13"})
+# ... from this many tokens per GEMM: at 2048 (Llama-3-8B B1 S2048) the fused path, whose W2 weight
+# gradient then runs the MFMA kernel on the row-major activation at K = 2048, is 1.8% slower in the
+# step; at 8192 (S8192 B1) 0.24% faster (profiles/r4/step_ab_llama3_8b_*_w13.log)
+NT_AUTO_MIN_TOKENS = 8192
 
 
 def _gemm_sites(v: str) -> frozenset:
@@ -244,7 +250,8 @@ def _nt_ok(a, b, site) -> bool:
         return False
     if not all(t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0 for t in (a, b)):
         return False
-    return not GEMM_AUTO or (a.size(0) // 256) * (b.size(0) // 256) >= 2 * _cus(a)
+    return not GEMM_AUTO or ((a.size(0) // 256) * (b.size(0) // 256) >= 2 * _cus(a)
+                             and a.size(0) >= NT_AUTO_MIN_TOKENS)
 
 
 def _mm_nt(a, b, site, b_t=None):

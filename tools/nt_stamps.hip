@@ -144,6 +144,15 @@ int main(int argc, char** argv) {
   // p31 has one sample fewer per wave than the others (no predecessor for the first chunk)
   printf("waves %zu chunks %.0f | per chunk: w1 %.0f p2 %.0f w2 %.0f p31 %.0f cycles\n", wait_per_chunk.size(), n,
          s[0] / n, s[1] / n, s[2] / n, s[3] / (n - wait_per_chunk.size()));
+  {  // per tile: prologue (DMA issue to chunk 0 landed), main loop, epilogue (stores issued and left)
+    double pro = 0, loop = 0, epi = 0, nt = 0;
+    for (long w = 0; w < nst / 8; ++w) {
+      const unsigned long long* o = &h[w * 8];
+      if (o[4] < 2) continue;
+      pro += (double)o[6]; loop += (double)o[5]; epi += (double)o[7]; nt += 1;
+    }
+    printf("per tile: prologue %.0f main loop %.0f epilogue %.0f cycles\n", pro / nt, loop / nt, epi / nt);
+  }
   printf("w1+w2 per chunk p10/p50/p90: %.0f %.0f %.0f | p2 p10/p50/p90: %.0f %.0f %.0f\n", pct(wait_per_chunk, 0.1),
          pct(wait_per_chunk, 0.5), pct(wait_per_chunk, 0.9), pct(p2_per_chunk, 0.1), pct(p2_per_chunk, 0.5),
          pct(p2_per_chunk, 0.9));
