@@ -585,10 +585,11 @@ void gemm_nt_(const at::Tensor& a, const at::Tensor& b, at::Tensor out, int64_t 
   const int cus = device_cus(a);
   const long nws = pra_gemm_nt_ws_floats((int)M, (int)N, (int)K, cus);
   at::Tensor ws, tickets;
-  if (nws > 0) {  // split tail scratch: exactly R * S partial tiles, from the caching allocator (graph-safe)
-    ws = at::empty({(int64_t)nws}, a.options().dtype(at::kFloat));
-    tickets = at::empty({(int64_t)pra_gemm_nt_ticket_count((int)M, (int)N, (int)K, cus)}, a.options().dtype(at::kInt));
-  }
+  // split tail scratch (exactly R * S partial tiles) and the tickets / tile counters, from the
+  // caching allocator (graph-safe)
+  if (nws > 0) ws = at::empty({(int64_t)nws}, a.options().dtype(at::kFloat));
+  const int ntk = pra_gemm_nt_ticket_count((int)M, (int)N, (int)K, cus);
+  if (ntk > 0) tickets = at::empty({(int64_t)ntk}, a.options().dtype(at::kInt));
   check(pra_gemm_nt(dt(a), (int)epi, a.data_ptr(), b.data_ptr(), out.data_ptr(), (int)M, (int)N, (int)K, a.stride(0),
                     b.stride(0), out.stride(0), c2, ldc2, (int)F, tabp, (int)S, (int)D, (int)nrot,
                     ws.defined() ? ws.data_ptr<float>() : nullptr, tickets.defined() ? tickets.data_ptr<int>() : nullptr,

@@ -1320,13 +1320,17 @@ struct AttnOptions {
   int dkdv_impl = -1;
   // dQ: -1/1 = region-pipelined bwd_dq_kernel<PIPE>, 0 = plain (padded non-causal keys: always plain)
   int dq_pipe = -1;
-  // pipelined dK/dV kernel, query heads per block: -1 = by grid size (dkdv_split), 1 = all of the
-  // kv head's Hq / Hkv heads in one block, n = Hq / Hkv / n heads per block plus an fp32 reduction
-  int dkdv_split = -1;
+  // pipelined dK/dV kernel, query heads per block: 1 = all of the kv head's Hq / Hkv heads in one
+  // block (default), n = Hq / Hkv / n heads per block plus an fp32 reduction, -1 = by grid size
+  // (dkdv_split) when no side-stream job waits for the window. Not by default: it pays only without
+  // the overlapped optimizer, and its fp32 partial sums would make the gradients depend on whether
+  // the optimizer overlaps (tests/test_xgmi_gpu.py compares the two bitwise)
+  int dkdv_split = 1;
   // two-wave dK/dV kernel (NW = 8, D = 128): 1 = K fragments held in registers (KREG), 0 = read from
-  // LDS, -1 = KREG unless a side-stream job waits for the dK/dV window (below)
-  // (B16 S2048 H32 bwd 2.387 -> 2.358 ms: profiles/r4/attn_ab_dkdv_kreg_b16.log)
-  int dkdv_kreg = -1;
+  // LDS (default), -1 = KREG unless a side-stream job waits for the dK/dV window (below)
+  // (B16 S2048 H32 bwd 2.387 -> 2.358 ms alone, but 1058.0 vs 1055.5 ms in the 7B step:
+  // profiles/r4/attn_ab_dkdv_kreg_b16.log, step_ab_7b_b16_kreg.log)
+  int dkdv_kreg = 0;
 };
 AttnOptions g_attn_opts;
 

@@ -63,7 +63,8 @@ __device__ __forceinline__ void dma16s_go(const void* sbase, uint32_t voff) {
 // s_waitcnt vmcnt(N) for a compile-time N
 template <int N>
 __device__ __forceinline__ void wait_vm() {
-  static_assert(N == 0 || N == 8 || N == 15 || N == 16 || N == 18 || N == 24 || N == 32, "add the count");
+  static_assert(N == 0 || N == 8 || N == 15 || N == 16 || N == 18 || N == 24 || N == 32 || N == 48, "add the count");
+  if constexpr (N == 48) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if constexpr (N == 15) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
   if constexpr (N == 18) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");

@@ -93,6 +93,9 @@ __device__ unsigned long long* pra_nt_stamp_out;
 // ST16: epilogue stores of 16 B (v_permlane16_swap pairs two 16-column blocks) instead of 8 B: per
 // 256x256 tile 11.8k instead of 16.1k cycles from loop end to stores retired; 32768x11008x4096
 // 1434 -> 1466 TF (profiles/r4/gemm_nt_st16_epilogue.log)
+// (Persistent workgroups walking per-XCD tile ranges through atomic counters, with the next tile's
+// prologue DMAs issued before the current tile's epilogue stores, measured 0.2-1.1% slower:
+// profiles/r4/gemm_nt_persistent_ab.log.)
 #ifndef PRA_NT_ST16
 #define PRA_NT_ST16 1
 #endif

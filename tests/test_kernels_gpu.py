@@ -279,6 +279,10 @@ def test_attention_bwd_dkdv_kernels(cuda, attn_opts, impl, B, S, Hq, Hkv, D, cau
     dq2, dk2, dv2 = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
     C.attn_bwd(q, k, v, o, do, lse, dq2, dk2, dv2, scale, causal)
     assert torch.equal(dq, dq2) and torch.equal(dk, dk2) and torch.equal(dv, dv2)
+    if impl == 2:  # K in registers reads the same values as K from LDS: bitwise the same gradients
+        attn_opts(dkdv_kreg=0)
+        C.attn_bwd(q, k, v, o, do, lse, dq2, dk2, dv2, scale, causal)
+        assert torch.equal(dq, dq2) and torch.equal(dk, dk2) and torch.equal(dv, dv2)
 
 
 @pytest.mark.parametrize("split", [2, 4])
@@ -312,9 +316,9 @@ def test_attention_bwd_dkdv_query_head_split(cuda, attn_opts, split, B, S, Hq, H
         dk32 = dk32.reshape(B * S, Hkv * D).clone()
         R.rope_inplace_2d(dk32, Hkv * D, tab, D, S, inverse=True)
         dk32 = dk32.view(B, S, Hkv, D)
-    # by-grid default (-1): split without a window job, unsplit when a side-stream job waits for the
-    # dK/dV window (mid_event)
-    attn_opts(dkdv_impl=1, dkdv_split=None)
+    # by grid (-1): split without a window job, unsplit when a side-stream job waits for the dK/dV
+    # window (mid_event)
+    attn_opts(dkdv_impl=1, dkdv_split=-1)
     for with_event in (False, True):
         ev = torch.cuda.Event()
         ev.record()
