@@ -308,11 +308,31 @@ __global__ __launch_bounds__(NTH) void gemm_nt_kernel(const T* __restrict__ A, c
         T* gp = C + row * ldc + n0 + 128 * wn + 4 * g4;
         T* up = gp + ep.F;
         uint2 gw[8], uw[8];
+        if constexpr (PRA_NT_ST16) {
+          // 16-B loads at the ST16 positions, swapped back to this lane's own 4 columns of blocks
+          // j and j + 1 (v_permlane16_swap is its own inverse on this pairing)
+          const long so = (16 * (g4 & 1) + 8 * (g4 >> 1)) - 4 * g4;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {  // all loads first: one wait for the whole row block
-          gw[j] = *reinterpret_cast<const uint2*>(gp + 16 * j);
-          uw[j] = *reinterpret_cast<const uint2*>(up + 16 * j);
+          for (int j = 0; j < 8; j += 2) {
+            const uint4 g8 = *reinterpret_cast<const uint4*>(gp + so + 16 * j);
+            const uint4 u8 = *reinterpret_cast<const uint4*>(up + so + 16 * j);
+            const auto g0 = __builtin_amdgcn_permlane16_swap(g8.x, g8.z, false, false);
+            const auto g1 = __builtin_amdgcn_permlane16_swap(g8.y, g8.w, false, false);
+            const auto u0 = __builtin_amdgcn_permlane16_swap(u8.x, u8.z, false, false);
+            const auto u1 = __builtin_amdgcn_permlane16_swap(u8.y, u8.w, false, false);
+            gw[j] = make_uint2(g0[0], g1[0]);
+            gw[j + 1] = make_uint2(g0[1], g1[1]);
+            uw[j] = make_uint2(u0[0], u1[0]);
+            uw[j + 1] = make_uint2(u0[1], u1[1]);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {  // all loads first: one wait for the whole row block
+            gw[j] = *reinterpret_cast<const uint2*>(gp + 16 * j);
+            uw[j] = *reinterpret_cast<const uint2*>(up + 16 * j);
+          }
         }
+        uint2 ogw[8], ouw[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           float g[4], u[4], og[4], ou[4];
@@ -327,8 +347,24 @@ __global__ __launch_bounds__(NTH) void gemm_nt_kernel(const T* __restrict__ A, c
             ou[e] = d * a;
             og[e] = dd * sg * (1.f + g[e] * (1.f - sg));
           }
-          *reinterpret_cast<uint2*>(gp + 16 * j) = make_uint2(pack_x2<T>(og[0], og[1]), pack_x2<T>(og[2], og[3]));
-          *reinterpret_cast<uint2*>(up + 16 * j) = make_uint2(pack_x2<T>(ou[0], ou[1]), pack_x2<T>(ou[2], ou[3]));
+          ogw[j] = make_uint2(pack_x2<T>(og[0], og[1]), pack_x2<T>(og[2], og[3]));
+          ouw[j] = make_uint2(pack_x2<T>(ou[0], ou[1]), pack_x2<T>(ou[2], ou[3]));
+          if constexpr (!PRA_NT_ST16) {
+            *reinterpret_cast<uint2*>(gp + 16 * j) = ogw[j];
+            *reinterpret_cast<uint2*>(up + 16 * j) = ouw[j];
+          }
+        }
+        if constexpr (PRA_NT_ST16) {
+          const long so = (16 * (g4 & 1) + 8 * (g4 >> 1)) - 4 * g4;
+#pragma unroll
+          for (int j = 0; j < 8; j += 2) {
+            const auto g0 = __builtin_amdgcn_permlane16_swap(ogw[j].x, ogw[j + 1].x, false, false);
+            const auto g1 = __builtin_amdgcn_permlane16_swap(ogw[j].y, ogw[j + 1].y, false, false);
+            const auto u0 = __builtin_amdgcn_permlane16_swap(ouw[j].x, ouw[j + 1].x, false, false);
+            const auto u1 = __builtin_amdgcn_permlane16_swap(ouw[j].y, ouw[j + 1].y, false, false);
+            *reinterpret_cast<uint4*>(gp + so + 16 * j) = make_uint4(g0[0], g1[0], g0[1], g1[1]);
+            *reinterpret_cast<uint4*>(up + so + 16 * j) = make_uint4(u0[0], u1[0], u0[1], u1[1]);
+          }
         }
       }
     }
