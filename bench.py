@@ -73,6 +73,15 @@ def launch_command(argv, gpus: int, env) -> list:
             "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + list(argv)
 
 
+def _gemm_sites(tokens):
+    """Which GEMM sites of this step run the hand-written MFMA kernels (ops/fused.py site rules)."""
+    from pyrecover_amd.ops import fused
+
+    nt = sorted(fused.GEMM_SITES) if (not fused.GEMM_AUTO or tokens >= fused.NT_AUTO_MIN_TOKENS) else []
+    wg = sorted(fused.WGRAD_SITES) if (not fused.WGRAD_AUTO or tokens >= fused.WGRAD_AUTO_MIN_TOKENS) else []
+    return {"nt_with_epilogues": nt, "weight_gradient": wg}
+
+
 def _adamw_fast() -> bool:
     from pyrecover_amd.optim import adamw
 
@@ -258,7 +267,8 @@ def main():
                        "optimizer": "AdamW (flat fused HIP)" + ("" if args.no_overlap_optimizer else
                                                                  f", overlapped with backward ({_opt_sched()})"),
                        "adamw_math": "hw rcp/sqrt (fast)" if _adamw_fast() else "torch _fused_adamw_ bit-exact",
-                       "weight_shadows": bool(getattr(flat, "t_mats", None))},
+                       "weight_shadows": bool(getattr(flat, "t_mats", None)),
+                       "hand_written_gemms": _gemm_sites(B * S)},
             "tokens_per_sec_per_gpu": round(tps / world, 2),
             "model_tflops_per_gpu": round(fpt * tps / world / 1e12, 2),
             "mfu_pct_vs_2.5PF": round(100 * fpt * tps / world / 2.5e15, 2),
