@@ -55,6 +55,7 @@ int main(int argc, char** argv) {
   const int M = argc > 1 ? atoi(argv[1]) : 32768, N = argc > 2 ? atoi(argv[2]) : 4096;
   const int K = argc > 3 ? atoi(argv[3]) : 4096;
   const double warm = argc > 4 ? atof(argv[4]) : 2.0;
+  const int epi = argc > 5 ? atoi(argv[5]) : 0;  // 0 plain, 1 SwiGLU (C = gu [M][N], a [M][N/2])
   const int cus = 256;
   __bf16 *A, *B, *C;
   CK(hipMalloc(&A, (size_t)M * K * 2));
@@ -83,8 +84,10 @@ int main(int argc, char** argv) {
     CK(hipMemset(st, 0, nst * 8));
   }
 #endif
+  __bf16* C2 = nullptr;
+  if (epi == 1) CK(hipMalloc(&C2, (size_t)M * (N / 2) * 2));
   auto launch = [&]() {
-    return pra_gemm_nt(pra::kBF16, 0, A, B, C, M, N, K, K, K, N, nullptr, 0, 0, nullptr, 0, 0, 0, ws, tk, cus, 0);
+    return pra_gemm_nt(pra::kBF16, epi, A, B, C, M, N, K, K, K, N, C2, N / 2, N / 2, nullptr, 0, 0, 0, ws, tk, cus, 0);
   };
   CK(launch());
   CK(hipDeviceSynchronize());
@@ -114,12 +117,13 @@ int main(int argc, char** argv) {
 #endif
   float* err;
   CK(hipMalloc(&err, 4096 * 4));
-  hipLaunchKernelGGL(sample_ref, dim3(64), dim3(64), 0, 0, A, B, C, M, N, K, err);
+  if (epi == 0) hipLaunchKernelGGL(sample_ref, dim3(64), dim3(64), 0, 0, A, B, C, M, N, K, err);
+  else CK(hipMemset(err, 0, 4096 * 4));  // (the SwiGLU epilogue is checked by tests/test_gemm_nt_gpu.py)
   std::vector<float> he(4096);
   CK(hipMemcpy(he.data(), err, 4096 * 4, hipMemcpyDeviceToHost));
   const float maxerr = *std::max_element(he.begin(), he.end());
-  printf("{\"kind\": \"%s\", \"M\": %d, \"N\": %d, \"K\": %d, \"warm_launches\": %d, \"ms\": %.4f, \"tflops\": %.1f, "
-         "\"max_rel_err_4096_samples\": %.5f}\n", kind, M, N, K, nwarm, ms, tf, maxerr);
+  printf("{\"kind\": \"%s\", \"epi\": %d, \"M\": %d, \"N\": %d, \"K\": %d, \"warm_launches\": %d, \"ms\": %.4f, "
+         "\"tflops\": %.1f, \"max_rel_err_4096_samples\": %.5f}\n", kind, epi, M, N, K, nwarm, ms, tf, maxerr);
   if (!(maxerr < 0.02f)) {
     fprintf(stderr, "WRONG RESULT\n");
     return 2;
