@@ -71,6 +71,9 @@ __device__ __forceinline__ i16x4 tr4(const T* tile, int byte_off) {
 // 1: each DMA group's M0 write first, its load last (no s_nop): 4096x4096x32768 1481-1509 -> 1514-1538
 // TF, 11008x4096x32768 1366-1376 -> 1407-1410 TF (tools/wgrad_variants.hip,
 // profiles/r4/wgrad_m0split_ab.log)
+#ifndef PRA_WG_SMAX
+#define PRA_WG_SMAX 2  // largest K-split of a partial last round (W2 at 4: 11% slower, profiles/r4/wgrad_w2_tail_split_ab.log)
+#endif
 #ifndef PRA_WG_M0SPLIT
 #define PRA_WG_M0SPLIT 1
 #endif
@@ -328,13 +331,13 @@ extern "C" {
 long pra_wgrad_ws_floats(int M, int N, int K, int cus) {
   using namespace pra::gm;
   const int nwg = (M / BM) * (N / BN);
-  const int S = pra::gemm_tail_split(nwg, cus, K / BK, 2);
+  const int S = pra::gemm_tail_split(nwg, cus, K / BK, PRA_WG_SMAX);
   return S > 1 ? (long)(nwg % cus) * S * BM * BN : 0;
 }
 int pra_wgrad_ticket_count(int M, int N, int K, int cus) {
   using namespace pra::gm;
   const int nwg = (M / BM) * (N / BN);
-  return pra::gemm_tail_split(nwg, cus, K / BK, 2) > 1 ? nwg % cus : 0;
+  return pra::gemm_tail_split(nwg, cus, K / BK, PRA_WG_SMAX) > 1 ? nwg % cus : 0;
 }
 
 hipError_t pra_wgrad_gemm(int dtype, const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb,
@@ -345,7 +348,7 @@ hipError_t pra_wgrad_gemm(int dtype, const void* A, const void* B, void* C, int 
   const int nwg = (M / BM) * (N / BN);
   // split the tiles of a partial last round S ways over K (S <= 2; 7B shapes: W13's 96 tail tiles
   // S = 2, 1.31 -> 1.40 PF; W2's 176 would need S = 4, measured slower, so unsplit)
-  const int Sx = pra::gemm_tail_split(nwg, cus, K / BK, 2);
+  const int Sx = pra::gemm_tail_split(nwg, cus, K / BK, PRA_WG_SMAX);
   const int n_split = Sx > 1 && ws && tickets ? nwg % cus : 0;
   const int S = n_split ? Sx : 1;
   // tickets are zeroed by a kernel, not hipMemsetAsync: replayed from a captured HIP graph
