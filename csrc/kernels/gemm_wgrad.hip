@@ -235,6 +235,8 @@ __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, c
   // epilogue: D[n][m] per 16 x 16 block: lane holds m = l & 15, n = 4 (l >> 4) + 0..3 (8 B)
   const int l16 = lane & 15, g4 = lane >> 4;
   auto store_c = [&](long m0, long n0) __attribute__((always_inline)) {
+    // (16-B stores through v_permlane16_swap, as gemm_nt.hip's ST16 epilogue, measured equal here: the
+    // epilogue is ~1% of a K = 32768 tile; profiles/r4/wgrad_st16_epilogue_ab.log)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       T* rowp = C + (m0 + 128 * wm + 16 * i + l16) * ldc + n0 + 128 * wn + 4 * g4;
