@@ -156,3 +156,26 @@ def test_gemm_nt_split_tail_under_hip_graph(cuda):
         ref = torch.empty_like(out)
         C.gemm_nt_(a, b, ref)
         assert torch.equal(out, ref)
+
+
+def test_auto_site_rule_runs_fused_swiglu_from_8192_tokens(cuda, monkeypatch):
+    """Default site list: the W1|W3 projection takes the NT kernel with the SwiGLU epilogue from
+    NT_AUTO_MIN_TOKENS tokens (and at least two rounds of 256x256 tiles), hipBLASLt below; the
+    MLP forward output is the same either way up to the GEMM's summation order."""
+    from pyrecover_amd.ops import fused
+
+    monkeypatch.setattr(fused, "GEMM_AUTO", True)
+    monkeypatch.setattr(fused, "GEMM_SITES", fused._NT_AUTO)
+    D, F = 1024, 128 * 22
+    w13 = _rnd(2 * F, D, scale=0.05)
+    for T, want in ((fused.NT_AUTO_MIN_TOKENS, True), (fused.NT_AUTO_MIN_TOKENS // 2, False)):
+        x = _rnd(T, D)
+        assert fused._nt_ok(x, w13, "w13") == want, T
+        assert not fused._nt_ok(x, w13, "o")  # plain sites stay on the library
+    x = _rnd(fused.NT_AUTO_MIN_TOKENS, D)
+    gu = torch.empty(x.size(0), 2 * F, dtype=x.dtype, device=x.device)
+    a = torch.empty(x.size(0), F, dtype=x.dtype, device=x.device)
+    _C().gemm_nt_(x, w13, gu, 1, a)
+    g, u = (x.float() @ w13.float().t()).split(F, dim=1)
+    ref = torch.nn.functional.silu(g) * u
+    assert _rel_err(a, ref) < 2e-2
