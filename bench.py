@@ -73,13 +73,15 @@ def launch_command(argv, gpus: int, env) -> list:
             "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + list(argv)
 
 
-def _gemm_sites(tokens):
+def _gemm_sites(tokens, dim):
     """Which GEMM sites of this step run the hand-written MFMA kernels (ops/fused.py site rules)."""
     from pyrecover_amd.ops import fused
 
-    nt = sorted(fused.GEMM_SITES) if (not fused.GEMM_AUTO or tokens >= fused.NT_AUTO_MIN_TOKENS) else []
+    nt_auto = tokens >= fused.NT_AUTO_MIN_TOKENS and dim >= fused.NT_AUTO_MIN_K
+    nt = sorted(fused.GEMM_SITES) if (not fused.GEMM_AUTO or nt_auto) else []
+    # weight-gradient sites also need one 256x256 output tile per CU (decided per GEMM at run time)
     wg = sorted(fused.WGRAD_SITES) if (not fused.WGRAD_AUTO or tokens >= fused.WGRAD_AUTO_MIN_TOKENS) else []
-    return {"nt_with_epilogues": nt, "weight_gradient": wg}
+    return {"nt_with_epilogues": nt, "weight_gradient_candidates": wg}
 
 
 def _adamw_fast() -> bool:
@@ -268,7 +270,7 @@ def main():
                                                                  f", overlapped with backward ({_opt_sched()})"),
                        "adamw_math": "hw rcp/sqrt (fast)" if _adamw_fast() else "torch _fused_adamw_ bit-exact",
                        "weight_shadows": bool(getattr(flat, "t_mats", None)),
-                       "hand_written_gemms": _gemm_sites(B * S)},
+                       "hand_written_gemms": _gemm_sites(B * S, cfg.dim)},
             "tokens_per_sec_per_gpu": round(tps / world, 2),
             "model_tflops_per_gpu": round(fpt * tps / world / 1e12, 2),
             "mfu_pct_vs_2.5PF": round(100 * fpt * tps / world / 2.5e15, 2),

@@ -213,6 +213,11 @@ _NT_AUTO = frozenset({"w13"})
 # gradient then runs the MFMA kernel on the row-major activation at K = 2048, is 1.8% slower in the
 # step; at 8192 (S8192 B1) 0.24% faster (profiles/r4/step_ab_llama3_8b_*_w13.log)
 NT_AUTO_MIN_TOKENS = 8192
+# ... and from this depth: a 256x256 tile's prologue + SwiGLU epilogue (~24k cycles) is measured
+# against a 4096-deep main loop (64 chunks, ~156k cycles); at K = 1024 it is a third of the tile,
+# and GPT-2-medium's step runs 6.2% slower with the fused path (104.5 vs 110.9 ms:
+# profiles/r4/step_ab_gpt2m_w13_r5l.log, profiles/r4/gemm_nt_swiglu_epilogue_stamps.log)
+NT_AUTO_MIN_K = 4096
 
 
 def _gemm_sites(v: str) -> frozenset:
@@ -251,7 +256,7 @@ def _nt_ok(a, b, site) -> bool:
     if not all(t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0 for t in (a, b)):
         return False
     return not GEMM_AUTO or ((a.size(0) // 256) * (b.size(0) // 256) >= 2 * _cus(a)
-                             and a.size(0) >= NT_AUTO_MIN_TOKENS)
+                             and a.size(0) >= NT_AUTO_MIN_TOKENS and a.size(1) >= NT_AUTO_MIN_K)
 
 
 def _mm_nt(a, b, site, b_t=None):

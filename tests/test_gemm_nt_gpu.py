@@ -160,21 +160,21 @@ def test_gemm_nt_split_tail_under_hip_graph(cuda):
 
 def test_auto_site_rule_runs_fused_swiglu_from_8192_tokens(cuda, monkeypatch):
     """Default site list: the W1|W3 projection takes the NT kernel with the SwiGLU epilogue from
-    NT_AUTO_MIN_TOKENS tokens (and at least two rounds of 256x256 tiles), hipBLASLt below; the
-    MLP forward output is the same either way up to the GEMM's summation order."""
+    NT_AUTO_MIN_TOKENS tokens and NT_AUTO_MIN_K model width (and at least two rounds of 256x256
+    tiles), hipBLASLt otherwise; the fused output matches the fp32 oracle."""
     from pyrecover_amd.ops import fused
 
     monkeypatch.setattr(fused, "GEMM_AUTO", True)
     monkeypatch.setattr(fused, "GEMM_SITES", fused._NT_AUTO)
-    D, F = 1024, 128 * 22
-    w13 = _rnd(2 * F, D, scale=0.05)
-    for T, want in ((fused.NT_AUTO_MIN_TOKENS, True), (fused.NT_AUTO_MIN_TOKENS // 2, False)):
-        x = _rnd(T, D)
-        assert fused._nt_ok(x, w13, "w13") == want, T
-        assert not fused._nt_ok(x, w13, "o")  # plain sites stay on the library
-    x = _rnd(fused.NT_AUTO_MIN_TOKENS, D)
-    gu = torch.empty(x.size(0), 2 * F, dtype=x.dtype, device=x.device)
-    a = torch.empty(x.size(0), F, dtype=x.dtype, device=x.device)
+    D, F, T = fused.NT_AUTO_MIN_K, 128 * 22, fused.NT_AUTO_MIN_TOKENS
+    w13 = _rnd(2 * F, D, scale=0.02)
+    x = _rnd(T, D)
+    assert fused._nt_ok(x, w13, "w13")
+    assert not fused._nt_ok(x, w13, "o")  # plain sites stay on the library
+    assert not fused._nt_ok(x[: T // 2], w13, "w13")  # too few tokens
+    assert not fused._nt_ok(x[:, : D // 4].contiguous(), w13[:, : D // 4].contiguous(), "w13")  # too shallow
+    gu = torch.empty(T, 2 * F, dtype=x.dtype, device=x.device)
+    a = torch.empty(T, F, dtype=x.dtype, device=x.device)
     _C().gemm_nt_(x, w13, gu, 1, a)
     g, u = (x.float() @ w13.float().t()).split(F, dim=1)
     ref = torch.nn.functional.silu(g) * u
