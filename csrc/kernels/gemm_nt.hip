@@ -7,9 +7,11 @@
 // transposed weight shadows so dX = dY W is NT too). Reference GEMM sites: model.py:171-177
 // (wq/wk/wv/wo), :264-269 (w1/w3/w2), :367 (output head).
 //
-// Machine (gemm_common.h): 256 x 256 tile, 4 waves of 128 x 128, 32-deep stages by LDS-DMA into a
-// 5-stage ring, counted vmcnt + raw s_barrier, v_mfma_f32_16x16x32, XCD-aware group-M order,
-// deterministic split-K tail. Operand tiles are [256 rows][32 k] (64-B rows) in LDS; MFMA operand
+// Machine (gemm_common.h): 256 x 256 tile, 4 waves of 128 x 128, v_mfma_f32_16x16x32, XCD-aware
+// group-M order, deterministic split-K tail, counted vmcnt + raw s_barrier. K % 64 == 0 (every
+// production shape): 64-deep chunks in two LDS buffers (run2b below, 128-B rows). K % 64 == 32:
+// 32-deep stages by LDS-DMA into a 5-stage ring (run). Operand tiles of the ring are [256 rows][32 k]
+// (64-B rows) in LDS; MFMA operand
 // fragments (16 rows x 32 k) are ONE ds_read_b128 per lane: lane l reads row l & 15, k 8(l >> 4)..+7,
 // exactly the MFMA operand map. The 16-B chunks of each row are XOR-swizzled by g((row >> 2) & 3),
 // g = {0, 2, 3, 1}, which makes every ds_read_b128 lane group cover the 16 slots of a bank row once
@@ -17,8 +19,8 @@
 // address instead.
 //
 // Orientation: acc = mfma(B fragment, A fragment), so a lane holds one output row m and 4
-// consecutive columns n in its 4 registers: RoPE pairs (2i, 2i+1) are in one lane, and a lane
-// writes 8 contiguous bytes per 16 x 16 block.
+// consecutive columns n in its 4 registers: RoPE pairs (2i, 2i+1) are in one lane; with ST16 two
+// 16 x 16 blocks are paired through v_permlane16_swap so each lane writes 16 contiguous bytes.
 //
 // Epilogues (EPI):
 //   0 plain:        C = A B^T (bf16/fp16 rounding once)
