@@ -28,7 +28,7 @@ from ..parallel.flat import FlatParams
 
 
 
-SHADOW_MIN_TOKENS = 8192  # see Transformer.flatten_
+SHADOW_MIN_TOKENS = 0  # see Transformer.flatten_
 
 class RMSNorm(nn.Module):
     """Parameter container + reference-compatible eager forward (reference model.py:25-49)."""
@@ -204,11 +204,10 @@ class Transformer(nn.Module):
         """Move all parameters/gradients into flat buffers (call after the final .to(device/dtype)).
 
         Transposed weight shadows (K-contiguous W^T for the data-gradient GEMMs, rewritten by the
-        optimizer) pay off when the GEMMs are large: +3.5% at 7B B16 (profiles/ab_weight_shadows_s7.log),
-        but at 2048 tokens per step the 2 B/param they add to the update traffic costs more than
-        the faster dgrad layout returns (Llama-3-8B B1: 107.5 vs 108.7 ms/step without them,
-        profiles/r4/). So they are kept from SHADOW_MIN_TOKENS tokens per micro-step (or when the
-        count is unknown); PRA_WEIGHT_SHADOWS=1/0 forces them on/off."""
+        optimizer): +3.5% at 7B B16 (profiles/ab_weight_shadows_s7.log), +5% at 7B B1 (99.1 vs
+        104.1-104.4 ms), -0.5% at Llama-3-8B B1 (108.1 vs 107.6 ms; profiles/r4/shadow_policy_b1/),
+        so they are on from SHADOW_MIN_TOKENS (0) tokens per micro-step. PRA_WEIGHT_SHADOWS=1/0
+        forces them on/off; PRA_WEIGHT_SHADOWS_HEAD=0 leaves the output head without one."""
         if self.flat is None:
             self.flat = FlatParams(self.fusion_groups())
             # optimizer-state indices follow model.parameters() order, as in the reference
@@ -218,19 +217,21 @@ class Transformer(nn.Module):
                 shadows = env == "1"
             else:
                 shadows = tokens_per_step is None or tokens_per_step >= SHADOW_MIN_TOKENS
-            for mats in self._gemm_weights() if shadows else []:
+            head = os.environ.get("PRA_WEIGHT_SHADOWS_HEAD", "1") == "1"
+            for mats in self._gemm_weights(head) if shadows else []:
                 self.flat.register_transposed(mats, (sum(p.shape[0] for p in mats), mats[0].shape[1]))
             # parameters written through the module API must refresh the transposed shadows
             self.register_load_state_dict_post_hook(lambda mod, keys: mod.flat.refresh_transposed())
         return self.flat
 
-    def _gemm_weights(self) -> List[List[nn.Parameter]]:
+    def _gemm_weights(self, head: bool = True) -> List[List[nn.Parameter]]:
         out = []
         for layer in self.layers.values():
             at, ff = layer.attention, layer.feed_forward
             out += [[at.wq.weight, at.wk.weight, at.wv.weight], [at.wo.weight], [ff.w1.weight, ff.w3.weight],
                     [ff.w2.weight]]
-        out.append([self.output.weight])
+        if head:
+            out.append([self.output.weight])
         return out
 
     def _weight_t(self, params: Sequence[nn.Parameter]) -> Optional[torch.Tensor]:
