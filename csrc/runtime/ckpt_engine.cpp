@@ -62,6 +62,9 @@ void register_ckpt_engine(py::module& m) {
       .def("md5_pending", &CkptEngine::md5_pending)
       .def("abandon_md5", &CkptEngine::abandon_md5, py::call_guard<py::gil_scoped_release>())
       .def("md5_max_seconds", &CkptEngine::md5_max_seconds)
+      .def("md5_min_bps", &CkptEngine::md5_min_bps)
+      .def("md5_pending_bytes", &CkptEngine::md5_pending_bytes)
+      .def("progress", &CkptEngine::progress)
       .def("wait", [](CkptEngine& e) {
         JobResult r;
         {
@@ -116,6 +119,10 @@ void register_ckpt_engine(py::module& m) {
            });
   m.attr("MD5PARTS_SEGMENT_BYTES") = py::int_(kSegBytes);
   m.def("md5_file", &md5_file, py::call_guard<py::gil_scoped_release>());
+  m.def("md5_probe_bps", &md5_probe_bps, py::arg("nbytes"), py::call_guard<py::gil_scoped_release>());
+  m.def("write_probe_bps", &write_probe_bps, py::arg("path"), py::arg("nbytes"), py::arg("threads") = kWriters,
+        py::arg("fsync") = true, py::call_guard<py::gil_scoped_release>());
+  m.attr("CKPT_WRITERS") = py::int_(kWriters);
   m.def("crc32_bytes", [](py::bytes b) {
     std::string s = b;
     return crc32_parallel(0, (const uint8_t*)s.data(), s.size());

@@ -49,6 +49,7 @@ extern "C" hipError_t pra_copy_d2d(void* dst, const void* src, long nbytes, hipS
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <utility>
 #include <vector>
 
@@ -298,10 +299,29 @@ struct JobResult {
   bool md5_deferred = false;  // the whole-file `.md5` sidecar is still being computed (flush())
 };
 
+struct CkptEngineIo {
+  // 0, or the errno of the first failed pwrite
+  static int try_pwrite_all(int fd, const uint8_t* b, size_t n, uint64_t pos) {
+    while (n) {
+      const ssize_t w = ::pwrite(fd, b, std::min<size_t>(n, 1u << 30), (off_t)pos);
+      if (w < 0) {
+        if (errno == EINTR) continue;
+        return errno;
+      }
+      b += w;
+      pos += (uint64_t)w;
+      n -= (size_t)w;
+    }
+    return 0;
+  }
+};
+
 // Streaming MD5 of an open file from its start (double-buffered reads on this thread, hashing
 // on the Md5Pipe thread). `cancel` (optional) is checked between reads: once set, the digest is
 // dropped and md5_fd throws.
-inline std::string md5_fd(int fd, const std::atomic<bool>* cancel = nullptr) {
+// `left` (optional) is decremented by the bytes hashed, `consumed` (optional) counts them.
+inline std::string md5_fd(int fd, const std::atomic<bool>* cancel = nullptr,
+                          std::atomic<int64_t>* left = nullptr, int64_t* consumed = nullptr) {
   Md5Pipe md5;
   constexpr size_t kBuf = 32u << 20;
   uint64_t pos = 0;
@@ -319,8 +339,87 @@ inline std::string md5_fd(int fd, const std::atomic<bool>* cancel = nullptr) {
     if (n == 0) break;
     md5.push_copy(buf->data(), (size_t)n);
     pos += (uint64_t)n;
+    if (left != nullptr) left->fetch_sub(n);
+    if (consumed != nullptr) *consumed += n;
   }
   return md5.finish();
+}
+
+// Throughput probes for the time-aware stop (the final checkpoint's cost is budgeted from the
+// bytes it will write and these rates before any save of the run has completed).
+// Single-stream MD5 over an in-memory buffer: the rate of the reference's whole-file `.md5`.
+inline double md5_probe_bps(uint64_t nbytes) {
+  nbytes = std::max<uint64_t>(nbytes, 1u << 20);
+  std::vector<uint8_t> buf(nbytes);
+  uint64_t x = 0x9e3779b97f4a7c15ull;
+  for (uint64_t i = 0; i + 8 <= nbytes; i += 8) {
+    x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+    std::memcpy(buf.data() + i, &x, 8);
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  EVP_MD_CTX* ctx = EVP_MD_CTX_new();
+  EVP_DigestInit_ex(ctx, EVP_md5(), nullptr);
+  EVP_DigestUpdate(ctx, buf.data(), buf.size());
+  unsigned char dig[EVP_MAX_MD_SIZE];
+  unsigned int len = 0;
+  EVP_DigestFinal_ex(ctx, dig, &len);
+  EVP_MD_CTX_free(ctx);
+  const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return (double)nbytes / std::max(s, 1e-9);
+}
+
+// Parallel write throughput through the archive writer's path: `threads` threads pwrite 64 MiB
+// aligned buffers of incompressible bytes at disjoint offsets of the probe file `path` (O_DIRECT
+// when the filesystem takes it), then fsync; the file is removed. Returns bytes/s.
+inline double write_probe_bps(const std::string& path, uint64_t nbytes, int threads, bool do_fsync) {
+  constexpr uint64_t kBuf = 64ull << 20;
+  threads = std::max(1, threads);
+  const uint64_t nchunks = std::max<uint64_t>(1, (nbytes + kBuf - 1) / kBuf);
+  const int fd = ::open(path.c_str(), O_CREAT | O_TRUNC | O_RDWR | O_CLOEXEC, 0644);
+  if (fd < 0) throw std::runtime_error("write probe: cannot open " + path + ": " + strerror(errno));
+  const int dfd = ::open(path.c_str(), O_WRONLY | O_CLOEXEC | O_DIRECT);
+  std::atomic<bool> direct{dfd >= 0};
+  std::atomic<uint64_t> next{0};
+  std::string err;
+  std::mutex err_mu;
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<std::thread> ws;
+  for (int t = 0; t < (int)std::min<uint64_t>((uint64_t)threads, nchunks); ++t)
+    ws.emplace_back([&, t] {
+      uint8_t* b = nullptr;
+      if (posix_memalign((void**)&b, 4096, kBuf) != 0) {
+        std::lock_guard<std::mutex> g(err_mu);
+        err = "write probe: alloc failed";
+        return;
+      }
+      uint64_t x = 0x243f6a8885a308d3ull ^ (uint64_t)t;
+      for (uint64_t i = 0; i + 8 <= kBuf; i += 8) {
+        x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+        std::memcpy(b + i, &x, 8);
+      }
+      for (uint64_t c; (c = next.fetch_add(1)) < nchunks;) {
+        int rc = EINVAL;
+        if (direct.load()) {
+          rc = CkptEngineIo::try_pwrite_all(dfd, b, kBuf, c * kBuf);
+          if (rc == EINVAL) direct = false;
+        }
+        if (rc == EINVAL) rc = CkptEngineIo::try_pwrite_all(fd, b, kBuf, c * kBuf);
+        if (rc != 0) {
+          std::lock_guard<std::mutex> g(err_mu);
+          err = std::string("write probe: ") + strerror(rc);
+          break;
+        }
+      }
+      ::free(b);
+    });
+  for (auto& w : ws) w.join();
+  if (dfd >= 0) ::close(dfd);
+  if (err.empty() && do_fsync && ::fsync(fd) != 0) err = "write probe: fsync failed";
+  const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  ::close(fd);
+  ::unlink(path.c_str());
+  if (!err.empty()) throw std::runtime_error(err);
+  return (double)(nchunks * kBuf) / std::max(s, 1e-9);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -469,6 +568,17 @@ class CkptEngine {
     wait_writer();
     running_ = true;
     result_ = JobResult{};
+    uint64_t est = 0;  // payload bytes (headers are added by the layout)
+    for (auto& it : items) {
+      est += it.n;
+      for (auto& rc : it.records) est += rc.nbytes;
+    }
+    prog_total_ = est;
+    prog_written_ = 0;
+    prog_hashed_ = 0;
+    const char* wm = std::getenv("PYRECOVER_WHOLE_MD5");
+    const bool whole = want_md5 && !(wm != nullptr && wm[0] == '0');
+    prog_md5_ = whole ? (defer_md5 ? 2 : 1) : 0;
     writer_ = std::thread([this, path, items = std::move(items), want_md5, do_fsync, defer_md5]() mutable {
       JobResult r;
       const auto t0 = std::chrono::steady_clock::now();
@@ -492,6 +602,20 @@ class CkptEngine {
   bool busy() {
     std::lock_guard<std::mutex> g(mu_);
     return running_;
+  }
+
+  // Progress of the current (or last) archive job: bytes of the file, bytes written, bytes of
+  // the inline whole-file MD5 hashed, and its mode (0 none, 1 inline, 2 deferred). The time-aware
+  // stop estimates the drain of an in-flight save from what is still to write.
+  std::tuple<uint64_t, uint64_t, uint64_t, int> progress() const {
+    return {prog_total_.load(), prog_written_.load(), prog_hashed_.load(), prog_md5_.load()};
+  }
+  // Bytes deferred digests still have to hash (queued and running), and the slowest completed
+  // digest's rate in bytes/s (0 if none of at least 64 MiB completed).
+  uint64_t md5_pending_bytes() const { return (uint64_t)std::max<int64_t>(0, md5st_->left.load()); }
+  double md5_min_bps() {
+    std::lock_guard<std::mutex> g(md5st_->mu);
+    return md5st_->min_bps;
   }
 
   JobResult wait() {
@@ -707,19 +831,8 @@ class CkptEngine {
     own(std::move(c));
   }
 
-  // 0, or the errno of the first failed pwrite
   static int try_pwrite_all(int fd, const uint8_t* b, size_t n, uint64_t pos) {
-    while (n) {
-      const ssize_t w = ::pwrite(fd, b, std::min<size_t>(n, 1u << 30), (off_t)pos);
-      if (w < 0) {
-        if (errno == EINTR) continue;
-        return errno;
-      }
-      b += w;
-      pos += (uint64_t)w;
-      n -= (size_t)w;
-    }
-    return 0;
+    return CkptEngineIo::try_pwrite_all(fd, b, n, pos);
   }
   static void pwrite_all(int fd, const uint8_t* b, size_t n, uint64_t pos) {
     if (const int e = try_pwrite_all(fd, b, n, pos))
@@ -786,6 +899,7 @@ class CkptEngine {
       r.items.push_back({start, off - start});
     }
     const uint64_t total = off;
+    prog_total_ = total;
     r.layout_seconds = std::chrono::duration<double>(clk::now() - t_layout).count() - r.stage_wait_seconds;
     const auto t_write = clk::now();
     const std::string tmp = path + ".tmp";
@@ -818,7 +932,12 @@ class CkptEngine {
         try {
           EVP_MD_CTX* ctx = EVP_MD_CTX_new();
           EVP_DigestInit_ex(ctx, EVP_md5(), nullptr);
-          for (auto& pc : pieces) EVP_DigestUpdate(ctx, pc.p, pc.n);
+          for (auto& pc : pieces)
+            for (uint64_t o = 0; o < pc.n; o += kHashStep) {
+              const uint64_t n = std::min<uint64_t>(kHashStep, pc.n - o);
+              EVP_DigestUpdate(ctx, pc.p + o, n);
+              prog_hashed_ += n;
+            }
           r.md5 = digest_hex(ctx);
           EVP_MD_CTX_free(ctx);
         } catch (const std::exception& e) {
@@ -871,6 +990,7 @@ class CkptEngine {
                 if (bounce) std::memcpy(bounce + (lo - c), src, hi - lo);
                 else pwrite_all(fd, src, hi - lo, lo);
                 if (want_md5 && !bounce) EVP_DigestUpdate(ctx, src, hi - lo);
+                if (!bounce) prog_written_ += hi - lo;
               }
               if (bounce) {
                 if (want_md5) EVP_DigestUpdate(ctx, bounce, e - c);
@@ -883,6 +1003,7 @@ class CkptEngine {
                   else if (rc != 0) throw std::runtime_error(std::string("ckpt_engine: write failed: ") + strerror(rc));
                 }
                 if (rc == EINVAL) pwrite_all(fd, bounce, e - c, c);  // buffered, exact length
+                prog_written_ += e - c;
               }
             }
             if (want_md5) r.seg_md5[s] = digest_hex(ctx);
@@ -934,9 +1055,12 @@ class CkptEngine {
       std::lock_guard<std::mutex> g(st->mu);
       ++st->running;
     }
+    const int64_t size = (int64_t)r.bytes;
+    st->left += size;
     r.md5_deferred = true;
     std::lock_guard<std::mutex> g(md5_th_mu_);
-    md5_th_.emplace_back([st, path, do_fsync] {
+    md5_th_.emplace_back([st, path, do_fsync, size] {
+      int64_t consumed = 0;  // this digest's bytes hashed (the rest leaves `left` at the end)
       std::string err;
       const auto t0 = std::chrono::steady_clock::now();
       bool done = false;
@@ -947,7 +1071,7 @@ class CkptEngine {
         std::string md5;
         try {
           if (::fstat(fd, &before) != 0) throw std::runtime_error("ckpt_engine: deferred md5: fstat failed");
-          md5 = md5_fd(fd, &st->cancel);
+          md5 = md5_fd(fd, &st->cancel, &st->left, &consumed);
         } catch (...) {
           ::close(fd);
           throw;
@@ -968,9 +1092,14 @@ class CkptEngine {
         if (!st->cancel.load()) err = e.what();
       }
       const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      st->left -= size - consumed;
       std::lock_guard<std::mutex> g2(st->mu);
       if (!err.empty()) st->error = err;
       if (done) st->max_seconds = std::max(st->max_seconds, sec);
+      if (done && size >= (int64_t)(64u << 20)) {
+        const double bps = (double)size / std::max(sec, 1e-9);
+        st->min_bps = st->min_bps > 0 ? std::min(st->min_bps, bps) : bps;
+      }
       --st->running;
     });
   }
@@ -1007,8 +1136,10 @@ class CkptEngine {
     std::mutex mu;
     int running = 0;
     double max_seconds = 0;  // longest completed deferred digest (feeds the time-aware budget)
+    double min_bps = 0;      // slowest completed digest of >= 64 MiB, bytes/s
     std::string error;
     std::atomic<bool> cancel{false};
+    std::atomic<int64_t> left{0};  // bytes still to hash over every queued / running digest
   };
   std::vector<std::thread> md5_th_;  // deferred whole-file digests
   std::mutex md5_th_mu_;
@@ -1016,6 +1147,9 @@ class CkptEngine {
   std::mutex mu_;
   bool running_ = false;
   JobResult result_;
+  static constexpr uint64_t kHashStep = 64ull << 20;
+  std::atomic<uint64_t> prog_total_{0}, prog_written_{0}, prog_hashed_{0};
+  std::atomic<int> prog_md5_{0};
 };
 
 // ------------------------------------------------------------------------------------------

@@ -323,7 +323,20 @@ class Checkpointer:
 # Background-write durations feed the time-aware stop: the FINAL checkpoint is written
 # synchronously (and first drains any in-flight write), so the stop threshold must budget the
 # full write time, not the ~ms an async save stalls training.
-WRITE_STATS = {"max_seconds": 0.0}
+WRITE_STATS: Dict[str, Any] = {"max_seconds": 0.0, "min_write_bps": 0.0, "min_inline_bps": 0.0}
+_RATE_MIN_BYTES = 64 << 20  # smaller jobs are overhead-dominated: their rates are not recorded
+
+
+def _record_rates(res: Dict[str, Any]):
+    """Per-byte rates of a completed archive job (slowest seen): plain writes, and writes that
+    computed the whole-file MD5 inline (their time is max(write, serial MD5))."""
+    nb = int(res.get("bytes", 0))
+    sec = float(res.get("write_seconds", 0.0)) + float(res.get("fsync_seconds", 0.0))
+    if nb < _RATE_MIN_BYTES or sec <= 0:
+        return
+    key = "min_inline_bps" if (res.get("md5") and not res.get("md5_deferred")) else "min_write_bps"
+    bps = nb / sec
+    WRITE_STATS[key] = bps if WRITE_STATS[key] <= 0 else min(WRITE_STATS[key], bps)
 
 
 @dataclass
@@ -342,7 +355,9 @@ class Job:
             if not self.result["ok"]:
                 raise RuntimeError(f"checkpoint write to {self.path} failed: {self.result['error']}")
             WRITE_STATS["max_seconds"] = max(WRITE_STATS["max_seconds"], float(self.result.get("seconds", 0.0)))
+            _record_rates(self.result)
             WRITE_STATS["last"] = {k: v for k, v in self.result.items() if k not in ("items", "records", "seg_md5")}
+            WRITE_STATS["jobs"] = WRITE_STATS.get("jobs", 0) + 1
             if self.on_done is not None:
                 self.on_done(self.result)
         return self.result
@@ -358,21 +373,110 @@ def max_write_seconds() -> float:
     return WRITE_STATS["max_seconds"]
 
 
-def max_digest_seconds() -> float:
-    """Longest completed deferred whole-file ``.md5`` digest of this process (0 if none yet): a
-    final checkpoint that computes its ``.md5`` inline takes about max(write, digest)."""
-    return max([c.engine.md5_max_seconds() for c in Checkpointer._instances.values()] + [0.0])
+class SaveCostModel:
+    """Predicted wall-clock of the time-aware FINAL save, and of the drain of an in-flight async
+    save, from bytes and measured rates.
+
+    The reference budgets a running maximum of completed save times (train.py:298-307), which
+    knows nothing until a save has completed: a job whose first save is the final one gets the
+    10 s prior whatever the model size. Here the final save costs
+
+        overhead + bytes / d2h + max(bytes / write rate, bytes / MD5 rate  [inline .md5 only])
+
+    with rates from a startup probe (:meth:`probe`: the archive writer's parallel O_DIRECT path
+    into the checkpoint directory, and the single-stream MD5 of the reference's whole-file
+    ``.md5``) until real saves report their own (slowest seen; a save that computed its digest
+    inline bounds the whole final save directly). ``bytes`` is what THIS rank writes (the whole
+    state for vanilla, ~1/W of it for sharded)."""
+
+    OVERHEAD_S = 2.0  # pickling, metadata, barriers, rename + sidecars
+
+    def __init__(self, state_bytes: int, inline_md5: bool, d2h_gbps: Optional[float] = None):
+        self.state_bytes = int(state_bytes)
+        self.inline_md5 = bool(inline_md5)
+        if d2h_gbps is None:
+            d2h_gbps = float(os.environ.get("PYRECOVER_D2H_GBPS", "20"))
+        self.d2h_bps = d2h_gbps * 1e9
+        self.probe_write_bps = 0.0
+        self.probe_md5_bps = 0.0
+
+    def probe(self, directory, write_bytes: Optional[int] = None, md5_bytes: int = 256 << 20):
+        """Measure the write rate into ``directory`` (a probe file of ``write_bytes``, default
+        clamp(state, 256 MiB, 2 GiB), removed afterwards) and the serial MD5 rate."""
+        n = _ext.native()
+        if write_bytes is None:
+            write_bytes = int(os.environ.get("PYRECOVER_CKPT_PROBE_BYTES", "0")) or \
+                min(max(self.state_bytes, 256 << 20), 2 << 30)
+        os.makedirs(str(directory), exist_ok=True)
+        import socket
+
+        path = os.path.join(str(directory), f".pyrecover_write_probe.{socket.gethostname()}.{os.getpid()}.tmp")
+        self.probe_write_bps = float(n.write_probe_bps(path, int(write_bytes), int(n.CKPT_WRITERS), True))
+        if self.inline_md5:
+            self.probe_md5_bps = float(n.md5_probe_bps(int(md5_bytes)))
+        return self
+
+    @property
+    def write_bps(self) -> float:
+        return WRITE_STATS["min_write_bps"] or self.probe_write_bps
+
+    @property
+    def md5_bps(self) -> float:
+        rates = [r for r in [self.probe_md5_bps] + [c.engine.md5_min_bps() for c in Checkpointer._instances.values()]
+                 if r > 0]
+        return min(rates) if rates else 0.0
+
+    @staticmethod
+    def _t(nbytes: float, bps: float) -> float:
+        return nbytes / bps if bps > 0 else 0.0
+
+    def final_seconds(self, nbytes: Optional[int] = None) -> float:
+        nb = self.state_bytes if nbytes is None else int(nbytes)
+        body = self._t(nb, self.write_bps)
+        if self.inline_md5:
+            body = max(body, self._t(nb, self.md5_bps), self._t(nb, WRITE_STATS["min_inline_bps"]))
+        return self.OVERHEAD_S + self._t(nb, self.d2h_bps) + body
+
+    def drain_seconds(self, final_budget: float) -> float:
+        """Extra seconds before the job can exit, beyond ``final_budget`` for the final save, that
+        in-flight work adds: the final save starts only once the in-flight archive is written
+        (the pinned pool is reused), and deferred whole-file digests (of the in-flight save, or
+        queued) must finish before exit. Estimated from the bytes still to write / hash."""
+        write_rem, digest_end = 0.0, 0.0
+        for c in Checkpointer._instances.values():
+            j = c.pending
+            busy = j is not None and j.result is None and c.engine.busy()
+            total, written, hashed, mode = c.engine.progress() if busy else (0, 0, 0, 0)
+            w = self._t(max(total - written, 0), self.write_bps)
+            if mode == 1:  # inline whole-file digest of the in-flight save
+                w = max(w, self._t(max(total - hashed, 0), self.md5_bps))
+            write_rem = max(write_rem, w)
+            pending = c.engine.md5_pending_bytes() + (total if mode == 2 else 0)
+            d = self._t(pending, self.md5_bps)
+            digest_end = max(digest_end, (w if mode == 2 else 0.0) + d)
+        return max(write_rem + final_budget, digest_end) - final_budget
 
 
-def inflight_remaining(estimate: float) -> float:
-    """Seconds the in-flight background writes still need, given an estimate of one full write."""
-    now = time.perf_counter()
-    rem = 0.0
-    for c in Checkpointer._instances.values():
-        j = c.pending
-        if j is not None and j.result is None and c.engine.busy():
-            rem = max(rem, estimate - (now - j.started))
-    return max(rem, 0.0)
+def drop_unverified(base: Path, keep: str) -> List[str]:
+    """After a time-aware stop whose final checkpoint carries its ``.md5``: remove older vanilla
+    checkpoints that have no ``.md5`` (a deferred digest cut short at the wall-clock limit), so
+    with ``--verify-checkpoints`` every checkpoint left on disk verifies with the reference's
+    loader (reference pyrecover/checkpoint.py:157-175). Returns the removed paths."""
+    removed = []
+    keep_step = ckpt_step(Path(keep))
+    for f in Path(base).glob("ckpt_*.pt"):
+        if str(f) == str(keep) or ckpt_step(f) >= keep_step or Path(str(f) + ".md5").exists():
+            continue
+        try:
+            f.unlink()
+            for side in (".md5parts",):
+                sp = Path(str(f) + side)
+                if sp.exists():
+                    sp.unlink()
+            removed.append(str(f))
+        except FileNotFoundError:
+            pass
+    return removed
 
 
 def flush_all(deadline: Optional[float] = None) -> bool:

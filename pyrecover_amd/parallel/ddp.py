@@ -261,7 +261,7 @@ class CommTimer:
             "exposed_comm_ms": round(exposed / n, 3),
             "allreduce_busy_ms": round(tot_ms, 3),
             "allreduce_gib": round(tot_b / 2**30, 3),
-            "allreduce_busbw_gbps": round(f * (tot_b / 1e9) / (tot_ms / 1e3), 1) if tot_ms > 0 else None,
+            "allreduce_busbw_gbps": round(f * (tot_b / 1e9) / (tot_ms / 1e3), 4) if tot_ms > 0 else None,
             "buckets": [{"mib": round(by / 2**20, 1), "ms": round(ms, 3),
                          "algbw_gbps": round(a, 1) if a else None, "busbw_gbps": round(f * a, 1) if a else None}
                         for by, ms, a in zip(self.bytes, busy, algbw)],

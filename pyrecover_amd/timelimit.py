@@ -6,8 +6,10 @@
 * :class:`TimeAwareStopper` - the reference's stop rule (train.py:164-232, 298-307, 334-337):
   stop when ``remaining < max_iter + max_ckpt + buffer`` with ``buffer = 10*iter + 2*ckpt``
   initially and ``5*max_iter + 1*max_ckpt`` after the first step; maxima are running maxima.
-  Extended with the in-flight async-checkpoint drain time and a signal path (SIGUSR1/SIGTERM,
-  e.g. ``#SBATCH --signal=B:USR1@120``) that requests a stop immediately.
+  Extended with a byte-based estimate of the final save (so the budget is sound before any save
+  has completed), the in-flight async-checkpoint drain time, the one-step-late distributed stop
+  flag, and a signal path (SIGUSR1/SIGTERM, e.g. ``#SBATCH --signal=B:USR1@120``) that requests a
+  stop immediately.
 * :func:`monitor_timelimit` - optional background thread that sets a flag near the deadline.
 """
 from __future__ import annotations
@@ -71,6 +73,20 @@ def get_remaining_time(end_time: Optional[float] = None, now: Optional[float] = 
 
 
 class TimeAwareStopper:
+    """The reference's stop rule plus the terms it lacks.
+
+    * ``max_iter`` / ``max_ckpt``: running maxima of observed iteration / save times, starting at
+      the ``--default-iter-time`` / ``--default-ckpt-time`` priors (reference train.py:167-176).
+    * ``ckpt_estimate``: the predicted cost of the FINAL save from the bytes it writes and measured
+      write / MD5 rates (:class:`pyrecover_amd.ckpt.core.SaveCostModel`). The reference only
+      learns a save's cost after one has completed, so a job whose first save is the final one is
+      budgeted at the 10 s prior however large the model; the budget uses
+      ``max(max_ckpt, ckpt_estimate)``.
+    * ``inflight_drain``: what an in-flight async save (and its deferred digest) still needs
+      before the final save can start / the job can exit.
+    * ``extra_iters``: iterations between rank 0's decision and the stop (1 with the one-step-late
+      distributed stop flag of the trainer).
+    """
     ITER_MULT_INIT, CKPT_MULT_INIT = 10, 2
     ITER_MULT, CKPT_MULT = 5, 1
 
@@ -79,17 +95,29 @@ class TimeAwareStopper:
                  install_signals: bool = False):
         self.max_iter = float(default_iter_time)
         self.max_ckpt = float(default_ckpt_time)
-        self.buffer = self.ITER_MULT_INIT * self.max_iter + self.CKPT_MULT_INIT * self.max_ckpt
+        self.ckpt_estimate = 0.0
         self.end_time = end_time
         self.clock = clock
         self.inflight_drain = 0.0  # seconds an in-flight async checkpoint still needs
+        self.extra_iters = 0
         self.signaled = False
+        self._stepped = False  # the reference switches to the steady-state buffer after step 1
         if install_signals:
             self.install_signal_handlers()
 
     @property
+    def ckpt_budget(self) -> float:
+        return max(self.max_ckpt, self.ckpt_estimate)
+
+    @property
+    def buffer(self) -> float:
+        if not self._stepped:
+            return self.ITER_MULT_INIT * self.max_iter + self.CKPT_MULT_INIT * self.ckpt_budget
+        return self.ITER_MULT * self.max_iter + self.CKPT_MULT * self.ckpt_budget
+
+    @property
     def threshold(self) -> float:
-        return self.max_iter + self.max_ckpt + self.buffer + self.inflight_drain
+        return (1 + self.extra_iters) * self.max_iter + self.ckpt_budget + self.buffer + self.inflight_drain
 
     def remaining(self) -> Optional[float]:
         if self.end_time is None:
@@ -105,13 +133,20 @@ class TimeAwareStopper:
     def update_iter(self, iter_time: float) -> bool:
         changed = iter_time > self.max_iter
         self.max_iter = max(self.max_iter, iter_time)
-        self.buffer = self.ITER_MULT * self.max_iter + self.CKPT_MULT * self.max_ckpt
+        self._stepped = True
         return changed
 
     def update_ckpt(self, ckpt_time: float) -> bool:
         changed = ckpt_time > self.max_ckpt
         self.max_ckpt = max(self.max_ckpt, ckpt_time)
         return changed
+
+    def set_ckpt_estimate(self, seconds: float) -> bool:
+        """The current byte-based prediction of the final save (not a running maximum: measured
+        rates replace the startup probe's as saves complete). True when the budget grew."""
+        before = self.ckpt_budget
+        self.ckpt_estimate = float(seconds)
+        return self.ckpt_budget > before + 1e-9
 
     def install_signal_handlers(self, signals=(signal.SIGUSR1, signal.SIGTERM)):
         def handler(signum, frame):

@@ -75,27 +75,48 @@ def _profiler_stop():
 
 
 class _StepTimer:
-    """Completed device-side step durations from events recorded at each step end (polled,
-    never blocking). ``record()`` returns the longest completed step seen since the last call."""
+    """Device-side step durations from events recorded at each step end (polled, never blocking).
+
+    The time-aware stop takes its iteration time from here, not from the host: the host runs
+    ahead of the GPU, so the host span of an ordinary step under-counts, and the span of a step
+    that synchronised (the log step's ``.item()``, the CSV) counts the drain of every queued
+    step. ``record()`` returns the longest step completed since the last call. ``gap()`` marks a
+    host-side pause that is not training time (a checkpoint save): the interval spanning it is
+    dropped. ``window()`` returns (mean, max, count) of the steps completed since the last
+    ``window()`` (the JSONL log)."""
 
     def __init__(self, enabled: bool):
         self.enabled = enabled
-        self.events = []
+        self.events = []  # (event, measure_from_previous)
         self.last = None
+        self._skip_next = False
+        self._win = []
+
+    def gap(self):
+        self._skip_next = True
 
     def record(self) -> float:
         if not self.enabled:
             return 0.0
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
-        self.events.append(ev)
+        self.events.append((ev, not self._skip_next))
+        self._skip_next = False
         longest = 0.0
-        while self.events and self.events[0].query():
-            e = self.events.pop(0)
-            if self.last is not None:
-                longest = max(longest, self.last.elapsed_time(e) / 1000.0)
+        while self.events and self.events[0][0].query():
+            e, measure = self.events.pop(0)
+            if self.last is not None and measure:
+                dt = self.last.elapsed_time(e) / 1000.0
+                longest = max(longest, dt)
+                self._win.append(dt)
             self.last = e
         return longest
+
+    def window(self):
+        w, self._win = self._win, []
+        if not w:
+            return None, None, 0
+        return sum(w) / len(w), max(w), len(w)
 
 
 class _StopFlagSync:
@@ -236,6 +257,9 @@ def train(args):
             log_rank0("--compile: no GPU, running eagerly")
     eager_steps_this_run = 0
     step_timer = _StepTimer(use_cuda)
+    # per-bucket collective timing for the JSONL (events only, no sync inside the step)
+    comm_timer = reducer.enable_comm_timing() if (is_dist and reducer is not None and args.metrics_jsonl) else None
+    ckpt_window = []  # host stall of each save issued since the last log line
     if args.async_checkpoint and int(args.checkpoint_frequency) > 0 and use_cuda:
         # params + AdamW moments (+ slack for the small entries); sharded saves need ~1/W of it.
         # Allocated now, while the GPU is idle: hipHostMalloc maps the pool into the GPU's page
@@ -287,7 +311,7 @@ def train(args):
         if final and not args.use_torch_distributed_ckpt:
             # the final (time-aware) checkpoint computes its whole-file .md5 inline, so the sidecar
             # the reference's verified load requires (pyrecover/checkpoint.py:157-175) exists when
-            # the save returns; the stop threshold budgets that digest (max_digest_seconds)
+            # the save returns; the stop threshold budgets that digest (SaveCostModel)
             kw["defer_md5"] = False
         save_ckpt_fn(model, optimizer, lr_scheduler, train_sampler, step, epoch, p,
                      max_keep=args.max_kept_checkpoints, verify=args.verify_checkpoints, is_distributed=is_dist,
@@ -308,6 +332,28 @@ def train(args):
         if stopper.end_time is None:
             log_rank0("Warning: SLURM_JOB_END_TIME is not set. Time-check logic will be skipped.")
         log_rank0(f"SLURM_JOB_END_TIME: {stopper.end_time}")
+    cost = None
+    if stopper is not None:
+        if is_dist:
+            stopper.extra_iters = 1  # every rank acts on rank 0's decision one step later (_StopFlagSync)
+        # what the final save writes on this rank: bf16/fp32 params + AdamW m, v (+ small entries)
+        state_bytes = 3 * flat.state_bytes()
+        if args.use_torch_distributed_ckpt:
+            state_bytes = -(-state_bytes // world_size)
+        inline_md5 = bool(args.verify_checkpoints) and not args.use_torch_distributed_ckpt
+        cost = ckcore.SaveCostModel(state_bytes, inline_md5)
+        if D.is_rank0() or args.use_torch_distributed_ckpt:
+            t0 = time.perf_counter()
+            try:
+                cost.probe(exp_ckpt_path)
+            except Exception as e:  # noqa: BLE001 - an unprobeable directory: the prior stays
+                log_rank0(f"Save-cost probe failed ({e}); budgeting the final save from --default-ckpt-time")
+            stopper.set_ckpt_estimate(cost.final_seconds())
+            log_rank0(f"Save-cost probe ({time.perf_counter() - t0:.2f}s): write {cost.write_bps / 1e9:.2f} GB/s"
+                      + (f", serial MD5 {cost.md5_bps / 1e9:.2f} GB/s" if inline_md5 else "")
+                      + f"; final checkpoint of {state_bytes / 2**30:.2f} GiB estimated at "
+                      f"{stopper.ckpt_estimate:.2f}s (budget {stopper.ckpt_budget:.2f}s, threshold "
+                      f"{stopper.threshold:.2f}s)")
     if args.resubmit != "none":
         resub.setup_resubmission(args.resubmit, args.resubmit_script,
                                  [a for a in os.environ.get("PYRECOVER_SCRIPT_ARGS", "").split() if a],
@@ -331,6 +377,7 @@ def train(args):
 
     train_dl_iterator = iter(train_dl)
     should_stop = False
+    local_stop = False  # rank 0's own time decision (latched; acted on via the broadcast when W > 1)
     stopped_for_time = False
     stop_sync = _StopFlagSync(device) if (stopper is not None and is_dist) else None
     log_rank0("Starting training!")
@@ -339,23 +386,21 @@ def train(args):
     loss = None
     while train_step < args.training_steps:
         train_step += 1
-        if stopper is not None:
-            # async saves stall training for ~ms, but the final save is synchronous and first
-            # drains the in-flight write: budget full write times
+        if cost is not None:
+            # async saves stall training for ~ms, but the final save is synchronous, first drains
+            # the in-flight write, and (with --verify-checkpoints) computes the serial whole-file
+            # MD5 inline: budget it from bytes and measured rates
             ckcore.poll_all()
-            wsec = ckcore.max_write_seconds()
-            if args.verify_checkpoints and not args.use_torch_distributed_ckpt:
-                # the final save's inline whole-file digest runs beside its write (serial MD5,
-                # ~0.9 GB/s): budget the longer of the two, as measured on earlier saves
-                wsec = max(wsec, ckcore.max_digest_seconds())
-            if stopper.update_ckpt(wsec):
-                log_rank0(f"Updated max_ckpt_time from background write/digest time: {stopper.max_ckpt:.2f}")
-            stopper.inflight_drain = ckcore.inflight_remaining(stopper.max_ckpt)
-        if stopper is not None and D.is_rank0() and stopper.should_stop():
-            should_stop = True
+            if stopper.set_ckpt_estimate(cost.final_seconds()):
+                log_rank0(f"Updated final checkpoint estimate from measured rates: {stopper.ckpt_estimate:.2f}s")
+            stopper.inflight_drain = cost.drain_seconds(stopper.ckpt_budget)
+        if stopper is not None and D.is_rank0() and not local_stop and stopper.should_stop():
+            local_stop = True
             rem = stopper.remaining()
             log_rank0(f"[TIME CHECK] Remaining time ({rem if rem is not None else float('nan'):.2f}s) < threshold "
-                      f"({stopper.threshold:.2f}s). should_stop set to True.")
+                      f"({stopper.threshold:.2f}s = {1 + stopper.extra_iters} x iter {stopper.max_iter:.2f}s + ckpt "
+                      f"{stopper.ckpt_budget:.2f}s + buffer {stopper.buffer:.2f}s + in-flight drain "
+                      f"{stopper.inflight_drain:.2f}s). should_stop set to True.")
         iter_start = time.perf_counter()
         if args.profile and args.profile_step_start == train_step:
             _profiler_start()
@@ -383,6 +428,8 @@ def train(args):
         if step_graph is not None and eager_steps_this_run >= args.compile_warmup_steps:
             loss = step_graph.step(*micro[0])  # fences the snapshot before the replay
         else:
+            if comm_timer is not None:
+                comm_timer.begin_step()
             optimizer.zero_grad()
             loss = None
             for m, (input_ids, labels) in enumerate(micro):
@@ -423,18 +470,25 @@ def train(args):
                       f"Training tokens per second (%): {100 * training_tps / tps:.2f} | MFU (%): {mfu:.2f} | "
                       f"TFLOPs: {tflops:.2f} | Tokens per second per GPU: {per_gpu:.2f}")
             if metrics_f is not None:
-                metrics_f.write(json.dumps({"step": train_step, "epoch": epoch, "loss": lval, "tokens_per_s": tps,
-                                            "tokens_per_s_per_gpu": per_gpu, "mfu_pct": mfu, "tflops_per_gpu": tflops,
-                                            "time": time.time()}) + "\n")
+                rec = {"step": train_step, "epoch": epoch, "loss": lval, "tokens_per_s": tps,
+                       "tokens_per_s_per_gpu": per_gpu, "mfu_pct": mfu, "tflops_per_gpu": tflops,
+                       "time": time.time()}
+                rec.update(_diagnostics(step_timer, device, comm_timer, world_size, ckpt_window, stopper))
+                metrics_f.write(json.dumps(rec) + "\n")
                 metrics_f.flush()
+            elif comm_timer is not None:
+                comm_timer.steps.clear()
+            ckpt_window.clear()
             ntokens_since_last_log = 0
             ntraining_tokens_since_last_log = 0
             time_last_log = time.perf_counter()
 
+        dev_step = step_timer.record()
         if stopper is not None:
-            # device time per step from events (no sync): the host-side span alone under-counts
-            # while the host runs ahead of the GPU
-            iter_time = max(time.perf_counter() - iter_start, step_timer.record())
+            # GPU: device time per step from events (no sync; never the host span, which
+            # under-counts while the host runs ahead and counts the drain of every queued step on
+            # a step that synchronised for logging). CPU: the host span (synchronous execution).
+            iter_time = dev_step if use_cuda else time.perf_counter() - iter_start
             if stopper.update_iter(iter_time):
                 log_rank0(f"Updated max_iter_time: {stopper.max_iter}")
             if train_step % args.logging_frequency == 0:
@@ -443,6 +497,8 @@ def train(args):
         if checkpoint_freq_steps > 0 and train_step % checkpoint_freq_steps == 0:  # 0 or -1: off
             log_rank0(f"Saving checkpoint to {ckpt_name(train_step)}")
             _, store_time = do_save(train_step, epoch)
+            step_timer.gap()
+            ckpt_window.append(store_time)
             total_checkpoint_store_time += store_time
             if stopper is not None and stopper.update_ckpt(store_time):
                 log_rank0(f"Updated max_ckpt_time: {stopper.max_ckpt}")
@@ -450,9 +506,9 @@ def train(args):
 
         if stopper is not None and is_dist:
             # rank 0's decision of the previous step (no per-step host sync)
-            should_stop = stop_sync.post(should_stop or stopper.signaled)
-        elif stopper is not None and stopper.signaled:
-            should_stop = True
+            should_stop = stop_sync.post(local_stop or stopper.signaled)
+        elif stopper is not None:
+            should_stop = local_stop or stopper.signaled
 
         if getattr(args, "stop_at_step", None) is not None and train_step == args.stop_at_step:
             should_stop = True
@@ -460,9 +516,11 @@ def train(args):
                 stopper = TimeAwareStopper(args.default_iter_time, args.default_ckpt_time, end_time=None)
         if stopper is not None and should_stop:
             log_rank0(f"[TIME CHECK] Saving final checkpoint to {ckpt_name(train_step, True)} before exit.")
-            _, store_time = do_save(train_step, epoch, final=True)
+            final_path, store_time = do_save(train_step, epoch, final=True)
             total_checkpoint_store_time += store_time
-            log_rank0(f"[TIME CHECK] Final checkpoint store completed in {store_time:.2f} seconds")
+            rem = stopper.remaining()
+            log_rank0(f"[TIME CHECK] Final checkpoint store completed in {store_time:.2f} seconds (estimated "
+                      f"{stopper.ckpt_estimate:.2f}s; {rem if rem is not None else float('nan'):.2f}s left)")
             stopped_for_time = True
             if args.resubmit != "none":
                 resub.maybe_resubmit(rank)
@@ -485,7 +543,12 @@ def train(args):
         end = getattr(stopper, "end_time", None)
         deadline = max((end - 10.0) if end else time.time() + 60.0, time.time() + 2.0)
         if not ckcore.flush_all(deadline=deadline):
-            log_rank0("[TIME CHECK] deferred .md5 digest abandoned at the wall-clock limit (.md5parts verify)")
+            log_rank0("[TIME CHECK] deferred .md5 digest abandoned at the wall-clock limit")
+            if args.verify_checkpoints and not args.use_torch_distributed_ckpt and D.is_rank0():
+                # every checkpoint kept under --verify-checkpoints carries its .md5
+                for f in ckcore.drop_unverified(exp_ckpt_path, str(final_path)):
+                    log_rank0(f"[TIME CHECK] removed {f}: its .md5 was not written before the limit "
+                              f"(the final checkpoint supersedes it)")
     else:
         ckcore.flush_all()
     total_checkpoint_store_time += time.perf_counter() - t0
@@ -501,6 +564,47 @@ def train(args):
     D.maybe_cleanup_distributed()
     return {"step": train_step, "epoch": epoch, "loss": float(loss.item()) if loss is not None else None,
             "stopped_early": should_stop}
+
+
+_CKPT_SEEN = {"jobs": 0}
+
+
+def _diagnostics(step_timer, device, comm_timer, world_size, ckpt_window, stopper) -> dict:
+    """Extra JSONL fields of a log step: device step time, HBM, exposed all-reduce
+    time and bus bandwidth, checkpoint stall / background write. Called right after the log
+    step's sync, so reading the events here does not stall the device queue."""
+    out = {}
+    mean, mx, n = step_timer.window()
+    out["device_step_ms"] = round(mean * 1e3, 3) if mean is not None else None
+    out["device_step_max_ms"] = round(mx * 1e3, 3) if mx is not None else None
+    if device.type == "cuda":
+        out["hbm_gib"] = round(torch.cuda.memory_allocated(device) / 2**30, 3)
+        out["hbm_peak_gib"] = round(torch.cuda.max_memory_allocated(device) / 2**30, 3)
+        out["hbm_reserved_gib"] = round(torch.cuda.memory_reserved(device) / 2**30, 3)
+    else:
+        out["hbm_gib"] = out["hbm_peak_gib"] = out["hbm_reserved_gib"] = None
+    if comm_timer is not None:
+        if comm_timer.cuda:
+            comm_timer.side.synchronize()  # its end events follow the collectives the step waited for
+        summ = comm_timer.summary(world_size)
+        comm_timer.steps.clear()
+        out["exposed_comm_ms"] = summ.get("exposed_comm_ms")
+        out["allreduce_busy_ms"] = summ.get("allreduce_busy_ms")
+        out["allreduce_busbw_gbps"] = summ.get("allreduce_busbw_gbps")
+    else:
+        out["exposed_comm_ms"] = out["allreduce_busy_ms"] = out["allreduce_busbw_gbps"] = None
+    out["ckpt_saves"] = len(ckpt_window)
+    out["ckpt_stall_s"] = round(sum(ckpt_window), 4)
+    jobs = ckcore.WRITE_STATS.get("jobs", 0)
+    last = ckcore.WRITE_STATS.get("last") if jobs != _CKPT_SEEN["jobs"] else None
+    _CKPT_SEEN["jobs"] = jobs
+    out["ckpt_write_s"] = round(float(last["seconds"]), 4) if last else None
+    out["ckpt_write_gib"] = round(float(last["bytes"]) / 2**30, 4) if last else None
+    if stopper is not None:
+        out["max_iter_time_s"] = round(stopper.max_iter, 4)
+        out["ckpt_budget_s"] = round(stopper.ckpt_budget, 3)
+        out["stop_threshold_s"] = round(stopper.threshold, 3)
+    return out
 
 
 def _clip_coef(flat, max_norm: float, pre_scale: float):

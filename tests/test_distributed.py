@@ -309,3 +309,27 @@ def test_xgmi_visibility_check_compares_device_identity():
     assert _hidden_ranks([("A", ["A"]), ("A", ["A"])]) == []
     assert _hidden_ranks([("A", ["A", "B"]), ("B", ["A", "B"])]) == []
     assert _hidden_ranks([("A", ["A", "B"]), ("B", ["B"])]) == [0]
+
+
+def test_metrics_jsonl_diagnostics_two_ranks(tmp_path):
+    """SURVEY §5.5 / reference train.py:283-296: every JSONL log record of a 2-rank gloo run carries
+    the device step time, HBM usage, the exposed all-reduce time with its bus bandwidth, and the
+    checkpoint stall / background write time (null where the quantity does not exist on CPU)."""
+    import json
+
+    ck = tmp_path / "ck"
+    jl = tmp_path / "m.jsonl"
+    argv = _argv(ck, 6, ["--distributed", "--checkpoint-frequency", "2", "--logging-frequency", "2",
+                         "--metrics-jsonl", str(jl), "--timeaware-checkpointing"])
+    _run(2, argv, tmp_path)
+    recs = [json.loads(ln) for ln in open(jl)]
+    assert [r["step"] for r in recs] == [1, 2, 4, 6]
+    keys = {"device_step_ms", "device_step_max_ms", "hbm_gib", "hbm_peak_gib", "hbm_reserved_gib",
+            "exposed_comm_ms", "allreduce_busy_ms", "allreduce_busbw_gbps", "ckpt_saves", "ckpt_stall_s",
+            "ckpt_write_s", "ckpt_write_gib", "max_iter_time_s", "ckpt_budget_s", "stop_threshold_s"}
+    for r in recs:
+        assert keys <= set(r), keys - set(r)
+        assert r["exposed_comm_ms"] is not None and r["exposed_comm_ms"] >= 0
+        assert r["allreduce_busy_ms"] > 0 and r["allreduce_busbw_gbps"] > 0
+    assert recs[2]["ckpt_saves"] == 1 and recs[2]["ckpt_stall_s"] > 0  # the save at step 4 ...
+    assert any(r["ckpt_write_s"] for r in recs[2:])  # ... and a completed background write

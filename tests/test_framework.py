@@ -120,8 +120,9 @@ def test_timeaware_training_stops_and_resumes(tmp_path, monkeypatch):
 
 def test_timeaware_final_checkpoint_carries_md5_and_budgets_digest(tmp_path, monkeypatch):
     """The time-aware final checkpoint is written with its whole-file .md5 (inline, not a deferred
-    digest that the wall-clock limit may cut short), and the stop threshold budgets the digest time
-    measured on earlier saves. Checked with the reference's own verification logic
+    digest that the wall-clock limit may cut short), the stop threshold budgets the final save's
+    predicted cost, and an older checkpoint whose deferred digest was cut short is not left on
+    disk without its .md5. Checked with the reference's own verification logic
     (pyrecover/checkpoint.py:157-171: md5 of the whole file == the sidecar's text)."""
     import hashlib
 
@@ -131,9 +132,9 @@ def test_timeaware_final_checkpoint_carries_md5_and_budgets_digest(tmp_path, mon
 
     end = time.time() + 300  # far above the initial 41 s threshold ...
     monkeypatch.setenv("SLURM_JOB_END_TIME", str(end))
-    # ... until the first save reports a 400 s whole-file digest (a big model's serial MD5)
-    monkeypatch.setattr(ckcore, "max_digest_seconds",
-                        lambda: 400.0 if ckcore.WRITE_STATS["max_seconds"] > 0 else 0.0)
+    # ... until the first save completes and the measured rates predict a 400 s final save
+    monkeypatch.setattr(ckcore.SaveCostModel, "final_seconds",
+                        lambda self, nbytes=None: 400.0 if ckcore.WRITE_STATS["max_seconds"] > 0 else 0.0)
     monkeypatch.setitem(ckcore.WRITE_STATS, "max_seconds", 0.0)
     monkeypatch.setattr(ckcore, "_FLUSH_AT_EXIT", [True])  # abandon_deferred_md5 clears it
 
@@ -152,6 +153,88 @@ def test_timeaware_final_checkpoint_carries_md5_and_budgets_digest(tmp_path, mon
     assert side.exists() and side.stat().st_mtime < end
     with open(final, "rb") as f:
         assert hashlib.md5(f.read()).hexdigest() == side.read_text()
+    for ck in (tmp_path / "default-exp").glob("ckpt_*.pt"):  # nothing unverifiable is kept
+        assert Path(str(ck) + ".md5").exists(), ck
+
+
+def test_timeaware_budget_sound_without_any_completed_save():
+    """No save has completed before the stop (BASELINE config 4 with --checkpoint-frequency 1000
+    and a 15-min limit). The reference budgets the final save at the 10 s prior; a 7B state
+    (37.65 GiB) written with its inline serial MD5 takes ~40 s. The byte-based estimate makes the
+    stop fire early enough; the prior alone would overrun the limit. Fake clock, 1.05 s steps."""
+    from pyrecover_amd.ckpt.core import SaveCostModel
+    from pyrecover_amd.timelimit import TimeAwareStopper
+
+    state = int(37.65 * 2**30)
+    cost = SaveCostModel(state, inline_md5=True, d2h_gbps=20.0)
+    cost.probe_write_bps, cost.probe_md5_bps = 4.2e9, 0.96e9  # what the probes measure on the box
+    est = cost.final_seconds()
+    actual_final = state / 1.0e9 + 1.0  # mocked: MD5 a little slower than probed, plus overhead
+    assert actual_final < est
+
+    def run(with_estimate: bool):
+        now = [0.0]
+        end = 600.0
+        st = TimeAwareStopper(1.0, 10.0, end_time=end, clock=lambda: now[0])
+        if with_estimate:
+            st.set_ckpt_estimate(est)
+        step = 0
+        while True:
+            step += 1
+            if st.should_stop():
+                break
+            now[0] += 1.05  # one step
+            st.update_iter(1.05)
+        return now[0] + 1.05 + actual_final, end  # the stop step, then the final save
+
+    finish, end = run(True)
+    assert finish < end, (finish, end)
+    finish_prior, _ = run(False)
+    assert finish_prior > end  # the reference's prior alone overruns
+
+
+def test_step_timer_ignores_host_drain_on_log_steps(monkeypatch):
+    """The iteration time is the device step, not the host span: a log step whose .item() drains
+    6 queued steps (6 s of host wait) still reports ~1 s, and the interval spanning a checkpoint
+    save's host pause is dropped."""
+    from pyrecover_amd import trainer
+
+    clock = {"dev": 0.0}
+    done_at = []
+
+    class FakeEvent:
+        def __init__(self, enable_timing=False):
+            self.t = None
+
+        def record(self):
+            clock["dev"] += 1.0  # every step takes 1.0 s of device time after the previous one
+            self.t = clock["dev"]
+            done_at.append(self)
+
+        def query(self):
+            return self.t <= clock["host"]
+
+        def elapsed_time(self, other):
+            return (other.t - self.t) * 1000.0
+
+    monkeypatch.setattr(trainer.torch.cuda, "Event", FakeEvent)
+    tm = trainer._StepTimer(True)
+    clock["host"] = 0.0
+    seen = []
+    for step in range(1, 13):
+        clock["host"] += 0.05  # host runs ahead
+        if step % 6 == 0:
+            clock["host"] = clock["dev"] + 1.0  # log step: .item() drains the queue
+        seen.append(tm.record())
+    assert max(seen) == pytest.approx(1.0)
+    tm.gap()  # a save pauses the host for 30 s: the device idles
+    clock["dev"] += 30.0
+    clock["host"] = clock["dev"] + 5
+    assert tm.record() == 0.0  # the interval spanning the pause is dropped
+    clock["host"] += 2.0
+    assert tm.record() == pytest.approx(1.0)
+    mean, mx, n = tm.window()
+    assert n >= 10 and mx == pytest.approx(1.0) and mean == pytest.approx(1.0)
 
 
 def test_slurm_duration_parse_and_remaining(monkeypatch):
@@ -260,32 +343,94 @@ def test_op_roctx_ranges_toggle():
 
 
 def test_time_aware_budgets_async_write_and_drain(monkeypatch):
-    """The stop threshold covers a full (synchronous) final write plus what an in-flight async
-    write still needs, not just the async stall."""
+    """The stop threshold covers the final save and what an in-flight async save still needs:
+    the rest of its write (from the engine's byte counters, not from a prior) and its deferred
+    whole-file digest."""
     import time as _t
 
     from pyrecover_amd.ckpt import core as ck
     from pyrecover_amd.timelimit import TimeAwareStopper
 
     st = TimeAwareStopper(1.0, 10.0, end_time=_t.time() + 1000)
+    st.update_iter(1.0)  # steady state: buffer = 5 iter + 1 ckpt
     base = st.threshold
-    monkeypatch.setitem(ck.WRITE_STATS, "max_seconds", 40.0)
-    assert st.update_ckpt(ck.max_write_seconds())
-    assert st.threshold == base + 30.0
+    cost = ck.SaveCostModel(40 * 10**9, inline_md5=True, d2h_gbps=40.0)
+    cost.probe_write_bps, cost.probe_md5_bps = 4e9, 1e9
+    monkeypatch.setitem(ck.WRITE_STATS, "min_write_bps", 0.0)
+    monkeypatch.setitem(ck.WRITE_STATS, "min_inline_bps", 0.0)
+    monkeypatch.setattr(ck.Checkpointer, "_instances", {})
+    assert cost.final_seconds() == pytest.approx(2.0 + 1.0 + 40.0)
+    assert st.set_ckpt_estimate(cost.final_seconds())
+    assert st.threshold == pytest.approx(base + 2 * (43.0 - 10.0))  # ckpt + buffer's ckpt term
 
     class _Eng:
         def busy(self):
             return True
 
+        def progress(self):  # 40 GB periodic save, 16 GB written, deferred digest
+            return (40 * 10**9, 16 * 10**9, 0, 2)
+
+        def md5_pending_bytes(self):
+            return 0
+
+        def md5_min_bps(self):
+            return 0.0
+
     class _C:
-        pending = ck.Job(ckpt=None, path="x", keepalive=None, on_done=None, started=_t.perf_counter() - 15.0)
+        pending = ck.Job(ckpt=None, path="x", keepalive=None, on_done=None, started=_t.perf_counter())
         engine = _Eng()
 
     monkeypatch.setattr(ck.Checkpointer, "_instances", {0: _C()})
-    rem = ck.inflight_remaining(st.max_ckpt)
-    assert 24.0 < rem <= 25.0
-    st.inflight_drain = rem
-    assert st.threshold > base + 30.0 + 24.0
+    drain = cost.drain_seconds(st.ckpt_budget)
+    # 24 GB left to write at 4 GB/s = 6 s; its 40 GB digest ends at 6 + 40 = 46 s, before the final
+    # save (6 + 43 = 49 s) finishes: the drain is the 6 s write
+    assert drain == pytest.approx(6.0)
+    st.inflight_drain = drain
+    assert st.threshold == pytest.approx(base + 66.0 + 6.0)
+    # a digest backlog longer than the final save extends the drain
+    monkeypatch.setattr(_Eng, "md5_pending_bytes", lambda self: 20 * 10**9)
+    assert cost.drain_seconds(st.ckpt_budget) == pytest.approx(6.0 + 60.0 - 43.0)
+
+
+def test_save_cost_probe_and_drop_unverified(tmp_path):
+    """The startup probes return positive rates (native write path into the checkpoint directory,
+    serial MD5), leave no probe file behind, and drop_unverified keeps only verified or newer
+    checkpoints."""
+    from pyrecover_amd import _ext
+    from pyrecover_amd.ckpt import core as ck
+
+    if not _ext.available():
+        pytest.skip("native extension not built")
+    cost = ck.SaveCostModel(64 << 20, inline_md5=True).probe(tmp_path, write_bytes=128 << 20, md5_bytes=16 << 20)
+    assert cost.probe_write_bps > 0 and cost.probe_md5_bps > 0
+    assert list(tmp_path.iterdir()) == []
+    for n, md5 in ((2, True), (4, False), (6, False)):
+        (tmp_path / f"ckpt_{n}.pt").write_bytes(b"x")
+        (tmp_path / f"ckpt_{n}.pt.md5parts").write_text("p")
+        if md5:
+            (tmp_path / f"ckpt_{n}.pt.md5").write_text("0" * 32)
+    (tmp_path / "ckpt_5_final.pt").write_bytes(b"x")
+    removed = ck.drop_unverified(tmp_path, str(tmp_path / "ckpt_5_final.pt"))
+    assert [Path(r).name for r in removed] == ["ckpt_4.pt"]
+    assert sorted(p.name for p in tmp_path.glob("*.pt")) == ["ckpt_2.pt", "ckpt_5_final.pt", "ckpt_6.pt"]
+    assert not (tmp_path / "ckpt_4.pt.md5parts").exists()
+
+
+def test_timeaware_stop_uses_final_save_estimate(tmp_path, monkeypatch):
+    """Trainer level: with no save before the stop, the threshold includes the predicted final
+    save (here 40 s), so a job with 70 s left stops at step 1 (the reference's 41 s prior would
+    keep going)."""
+    from pyrecover_amd.ckpt import core as ckcore
+    from pyrecover_amd.cli import get_args
+    from pyrecover_amd.trainer import train
+
+    monkeypatch.setenv("SLURM_JOB_END_TIME", str(time.time() + 70))
+    monkeypatch.setattr(ckcore.SaveCostModel, "final_seconds", lambda self, nbytes=None: 40.0)
+    base = ["--model-preset", "llama-micro", "--synthetic-data", "--sequence-length", "128", "--batch-size", "2",
+            "--training-steps", "20", "--checkpoint-dir", str(tmp_path), "--checkpoint-frequency", "-1",
+            "--model-dtype", "fp32", "--num-workers", "0", "--timeaware-checkpointing"]
+    r = train(get_args(base))
+    assert r["stopped_early"] and r["step"] == 1
 
 
 def test_loss_csv_log_line_and_metrics_jsonl(tmp_path, caplog):

@@ -17,13 +17,20 @@ ARGS="--model-preset llama2-7b --n-layers ${TA_LAYERS:-8} --synthetic-data --seq
   --max-kept-checkpoints ${TA_KEEP:-2} --resubmit requeue --num-workers 2"
 export SLURM_JOB_END_TIME=$(( $(date +%s) + ${LIMIT_S:-90} ))
 timeout -k 10 400 python train.py $ARGS > $OUT/run1.log 2>&1 || { tail -40 $OUT/run1.log; exit 1; }
-grep -E "TIME CHECK|final|Checkpoint|resubmi|Training completed|stopp" $OUT/run1.log | tail -15
-ls -la $CK/ta > $OUT/ckpts_after_run1.txt
+grep -E "TIME CHECK|final|Checkpoint|resubmi|Training completed|stopp|probe|max_iter" $OUT/run1.log | tail -20
+ls -la --time-style=+%s $CK/ta > $OUT/ckpts_after_run1.txt
+# soundness: the final checkpoint and its .md5 exist before the (simulated) wall-clock limit
+fin=$(ls $CK/ta/ckpt_*_final.pt 2>/dev/null | head -1)
+if [ -n "$fin" ] && [ -f "$fin.md5" ]; then
+  echo "final .md5 written at $(stat -c %Y $fin.md5), limit $SLURM_JOB_END_TIME, margin $(( SLURM_JOB_END_TIME - $(stat -c %Y $fin.md5) )) s" | tee $OUT/final_md5_margin.txt
+else
+  echo "NO final checkpoint with .md5" | tee $OUT/final_md5_margin.txt
+fi
 unset SLURM_JOB_END_TIME
 timeout -k 10 600 python train.py $ARGS --resume-from-checkpoint latest > $OUT/run2.log 2>&1 \
   || { tail -40 $OUT/run2.log; exit 1; }
 grep -E "Resum|loaded|Checkpoint load|Step: ${TA_STEPS:-1500}|Training completed" $OUT/run2.log | tail -10
-ls -la $CK/ta > $OUT/ckpts_after_run2.txt
+ls -la --time-style=+%s $CK/ta > $OUT/ckpts_after_run2.txt
 if [ "${TA_REF:-0}" = "1" ]; then
   # bit-exact resume check: an uninterrupted run to the same step, final checkpoints compared
   last=$CK/ta/ckpt_${TA_STEPS:-1500}.pt
