@@ -547,6 +547,9 @@ void gemm_nt_(const at::Tensor& a, const at::Tensor& b, at::Tensor out, int64_t 
               "gemm_nt: bf16/fp16 operands of one dtype");
   TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 32 == 0 && K > 0, "gemm_nt: M, N % 256 and K % 32");
   TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && out.stride(0) % 8 == 0, "gemm_nt: 16-B rows");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+              "gemm_nt: 16-B aligned operands (the epilogue stores 16 B per lane)");
   TORCH_CHECK(epi >= 0 && epi <= 3, "gemm_nt: epi in 0..3");
   int64_t F = 0;
   void* c2 = nullptr;
@@ -565,6 +568,7 @@ void gemm_nt_(const at::Tensor& a, const at::Tensor& b, at::Tensor out, int64_t 
     TORCH_CHECK(out2->scalar_type() == a.scalar_type() && out2->size(0) == M && out2->size(1) == F &&
                     out2->stride(0) % 8 == 0,
                 "gemm_nt swiglu: a [M, F]");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(out2->data_ptr()) % 16 == 0, "gemm_nt swiglu: 16-B aligned out2");
     c2 = out2->data_ptr();
     ldc2 = out2->stride(0);
   }

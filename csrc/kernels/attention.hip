@@ -33,6 +33,14 @@
 
 #include <type_traits>
 
+// Variant switches (tools/attn_variants.sh builds the standalone harness per setting)
+#ifndef PRA_FWD_MINBLK
+#define PRA_FWD_MINBLK 2
+#endif
+#ifndef PRA_FWD_PRESCALE
+#define PRA_FWD_PRESCALE 0
+#endif
+
 namespace pra {
 namespace attn {
 
@@ -445,7 +453,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_kernel(const T* __restrict__ Q
 // wave's only diagonal tile is its last one.
 // ======================================================================================
 template <typename T, int D, bool CAUSAL, int NW>
-__global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const T* __restrict__ Q, const T* __restrict__ K,
+__global__ __launch_bounds__(NW * 64, PRA_FWD_MINBLK) void fwd_p_kernel(const T* __restrict__ Q, const T* __restrict__ K,
                                                            const T* __restrict__ V, T* __restrict__ O,
                                                            float* __restrict__ LSE, int S, int Hq, int Hkv, long ldq,
                                                            long ldk, long ldv, long ldo, float scale_log2, float thr) {
@@ -477,8 +485,16 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const T* __restrict__
   V8<T> qf[NKS];
   const int qrow = qw + l32;
 #pragma unroll
-  for (int ks = 0; ks < NKS; ++ks)
+  for (int ks = 0; ks < NKS; ++ks) {
     qf[ks] = qrow < S ? *reinterpret_cast<const V8<T>*>(Qb + (long)qrow * ldq + 16 * ks + 8 * h2) : V8<T>{};
+#if PRA_FWD_PRESCALE
+    // Q pre-multiplied by scale * log2(e) (rounded to T: ~2^-9 relative per element, ~0.1% on P at
+    // D = 128), so the scores come out of the MFMA in log2 units, already minus the running max
+    // (the accumulator starts at -m: negm below): the softmax needs one v_exp per score, no FMA
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qf[ks][j] = (T)((float)qf[ks][j] * scale_log2);
+#endif
+  }
 
   f32x16 o[NDB];
 #pragma unroll
@@ -514,8 +530,9 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const T* __restrict__
     float mx = -INFINITY;
 #pragma unroll
     for (int r = 0; r < 16; ++r) mx = fmaxf(mx, fmaxf(s0[r], s1[r]));
-    return half_max(mx) * scale_log2;
+    return PRA_FWD_PRESCALE ? half_max(mx) : half_max(mx) * scale_log2;
   };
+  f32x16 negm;  // -m_i in every register: the initial accumulator of a score tile (PRA_FWD_PRESCALE)
 
   f32x16 c0 = f32x16{}, c1 = f32x16{};  // scores of the tile being finished (two 32-key halves)
   if (lastw >= 0) {
@@ -527,7 +544,16 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const T* __restrict__
     }
     if (CAUSAL && lastw == 0) mask(c0, c1, 0);
     m_i = rowmax(c0, c1);
+#if PRA_FWD_PRESCALE
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      c0[r] -= m_i;
+      c1[r] -= m_i;
+    }
+#endif
   }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) negm[r] = -m_i;
 
   // the ring slot of tile t is a compile-time constant (loop unrolled by 3), so every LDS operand
   // address is a lane-constant base plus an immediate offset
@@ -553,9 +579,22 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const T* __restrict__
         constexpr int RA = NKS, EA = NEA / RA;  // phase A: regions / softmax elements per region
         constexpr int RB = 2 * NDB, EB = 32 / RB;
         constexpr int EBX = (32 - NEA) / (RB / 2);  // phase B exponentials per region
+#if PRA_FWD_PRESCALE
+        f32x16 n0 = negm, n1 = negm;
+#else
         f32x16 n0 = f32x16{}, n1 = f32x16{};
+#endif
         float rs = 0.f, mx = -INFINITY;
         auto expo = [&](int e) {  // element e of the 32 scores of tile t
+#if PRA_FWD_PRESCALE
+          if (e < 16) {
+            c0[e] = fexp2(c0[e]);
+            rs += c0[e];
+          } else {
+            c1[e - 16] = fexp2(c1[e - 16]);
+            rs += c1[e - 16];
+          }
+#else
           if (e < 16) {
             c0[e] = fexp2(fmaf(c0[e], scale_log2, -m_i));
             rs += c0[e];
@@ -563,6 +602,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const T* __restrict__
             c1[e - 16] = fexp2(fmaf(c1[e - 16], scale_log2, -m_i));
             rs += c1[e - 16];
           }
+#endif
         };
         // phase A: S(t+1) | exp, row sum of tile t
         V8<T> a0 = lo.rowk(Kn, 0, 0), a1 = lo.rowk(Kn, 32, 0);
@@ -618,6 +658,23 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const T* __restrict__
           __builtin_amdgcn_sched_barrier(0);
         }
         if (NEXT) {
+#if PRA_FWD_PRESCALE
+          mx = half_max(mx);  // max growth over m_i (the scores are relative to it)
+          if (!__all(mx <= thr)) {  // deferred rescale (tile t's P.V is already in O)
+            const float dlt = fmaxf(mx, 0.f);
+            const float alpha = fexp2(-dlt);
+            l_i *= alpha;
+#pragma unroll
+            for (int i = 0; i < NDB; ++i) o[i] *= alpha;
+            m_i += dlt;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              n0[r] -= dlt;
+              n1[r] -= dlt;
+              negm[r] = -m_i;
+            }
+          }
+#else
           mx = half_max(mx) * scale_log2;
           if (!__all(mx <= m_i + thr)) {  // deferred rescale (tile t's P.V is already in O)
             const float m_new = fmaxf(m_i, mx);
@@ -627,6 +684,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fwd_p_kernel(const T* __restrict__
             for (int i = 0; i < NDB; ++i) o[i] *= alpha;
             m_i = m_new;
           }
+#endif
           c0 = n0;
           c1 = n1;
         }
@@ -1501,8 +1559,10 @@ hipError_t pra_attn_fwd(int dtype, const void* q, const void* k, const void* v, 
                             ldk, ldv, ldo, scale, causal, skv, st);
   if (dtype == pra::kBF16)
     return attn_fwd_t<__bf16>(q, k, v, o, lse, B, S, Hq, Hkv, D, ldq, ldk, ldv, ldo, scale, causal, skv, st);
+#if !PRA_ATTN_HARNESS
   if (dtype == pra::kF16)
     return attn_fwd_t<_Float16>(q, k, v, o, lse, B, S, Hq, Hkv, D, ldq, ldk, ldv, ldo, scale, causal, skv, st);
+#endif
   return hipErrorInvalidValue;
 }
 
@@ -1521,9 +1581,11 @@ hipError_t pra_attn_bwd(int dtype, const void* q, const void* k, const void* v, 
   if (dtype == pra::kBF16)
     return attn_bwd_t<__bf16>(q, k, v, o, dout, lse, delta, dq, dk, dv, B, S, Hq, Hkv, D, ldq, ldk, ldv, ldo, lddo,
                               lddq, lddk, lddv, scale, causal, skv, rope_tab, mid_event, st);
+#if !PRA_ATTN_HARNESS
   if (dtype == pra::kF16)
     return attn_bwd_t<_Float16>(q, k, v, o, dout, lse, delta, dq, dk, dv, B, S, Hq, Hkv, D, ldq, ldk, ldv, ldo, lddo,
                                 lddq, lddk, lddv, scale, causal, skv, rope_tab, mid_event, st);
+#endif
   return hipErrorInvalidValue;
 }
 

@@ -77,6 +77,9 @@ __global__ __launch_bounds__(256) void copy1_kernel(unsigned char* __restrict__ 
 extern "C" hipError_t pra_copy_d2d(void* dst, const void* src, long nbytes, hipStream_t s) {
   if (nbytes <= 0) return hipSuccess;
   const bool al = reinterpret_cast<uintptr_t>(dst) % 16 == 0 && reinterpret_cast<uintptr_t>(src) % 16 == 0;
+  // a misaligned region would otherwise go through the 1-byte kernel whole: the runtime's copy
+  // engine path is faster there (checkpoint regions are 64-B aligned, so this is a fallback)
+  if (!al && nbytes > 4096) return hipMemcpyAsync(dst, src, (size_t)nbytes, hipMemcpyDeviceToDevice, s);
   const long n16 = al ? nbytes / 16 : 0;
   if (n16 > 0) {
     long blocks = (n16 + 255) / 256;

@@ -96,11 +96,12 @@ def _apply_options(mod, env: dict) -> None:
 def set_attn_options(**kw) -> dict:
     """Set attention kernel selection knobs (fwd_pipe, fwd_thr, dkdv_impl, dq_pipe, dkdv_split, dkdv_kreg); keys left out
     keep their value, ``None`` restores the default. Returns the previous settings."""
+    mod = native()  # loads the extension and applies the PYRECOVER_ATTN_* values first
     prev = dict(_attn_opts)
     new = {}
     for k, v in kw.items():
         if k not in _ATTN_DEFAULTS:
             raise KeyError(f"unknown attention option {k!r}")
         new[k] = _ATTN_DEFAULTS[k] if v is None else type(_ATTN_DEFAULTS[k])(v)
-    _apply_options(native(), new)
+    _apply_options(mod, new)
     return prev

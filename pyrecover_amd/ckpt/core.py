@@ -102,6 +102,7 @@ def restore_rng_from(ps: Optional[Dict[str, Any]]):
     """Restore this rank's RNG from a checkpoint's ``pyrecover_state``: its own entry of
     ``rng_per_rank`` when the world size matches, else the saving process's ``rng``."""
     ps = ps or {}
+    warn_reduction_change(ps)
     per = ps.get("rng_per_rank")
     if per:
         per = [per[k] for k in sorted(per, key=int)] if isinstance(per, dict) else list(per)
@@ -113,6 +114,19 @@ def restore_rng_from(ps: Optional[Dict[str, Any]]):
         restore_rng_state(per[rank])
     else:
         restore_rng_state(ps.get("rng"))
+
+
+def warn_reduction_change(ps: Optional[Dict[str, Any]]) -> List[str]:
+    """Warn when the checkpoint was written under different gradient-reduction settings (world size,
+    backend, RCCL algorithm / protocol / channels): the resumed run is then not guaranteed to be
+    bit-identical to an uninterrupted one. PYRECOVER_RCCL_DETERMINISTIC=1 pins them."""
+    from ..parallel import dist as _dist
+
+    diffs = _dist.compare_rccl_order((ps or {}).get("reduction"))
+    if diffs and _dist.is_rank0():
+        logger.warning("checkpoint was written with different gradient-reduction settings; the resumed run "
+                       "may not be bit-identical to an uninterrupted one: " + "; ".join(diffs))
+    return diffs
 
 
 def build_state(model, optimizer, lr_scheduler=None, sampler=None, step: int = 0, epoch: Optional[int] = None,
@@ -131,7 +145,10 @@ def build_state(model, optimizer, lr_scheduler=None, sampler=None, step: int = 0
         state["lr_scheduler"] = lr_scheduler.state_dict()
     if sampler is not None and hasattr(sampler, "set_state"):
         state["sampler_state"] = sampler.state_dict()
-    ps = {"format": "pyrecover_amd/1", "rng": capture_rng_state(), "saved_at": time.time()}
+    from ..parallel import dist as _dist
+
+    ps = {"format": "pyrecover_amd/1", "rng": capture_rng_state(), "saved_at": time.time(),
+          "reduction": _dist.rccl_order_settings()}
     if torch.distributed.is_available() and torch.distributed.is_initialized():
         ps["world_size"] = torch.distributed.get_world_size()
     if rng_per_rank is not None:
@@ -272,8 +289,19 @@ class Checkpointer:
             logger.info(f"checkpoint snapshot: {nbytes / 2**30:.1f} GiB HBM bounce buffer does not fit "
                         f"({free / 2**30:.1f} GiB free): direct D2H, the next update waits for it")
             return None
-        self._hbm = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        try:
+            self._hbm = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        except torch.OutOfMemoryError:
+            logger.info(f"checkpoint snapshot: {nbytes / 2**30:.1f} GiB HBM bounce buffer allocation failed: "
+                        f"direct D2H, the next update waits for it")
+            return None
         return self._hbm
+
+    def release_hbm(self):
+        """Free the bounce buffer (OOM recovery: training allocations take precedence over the
+        two-hop snapshot; the next save re-checks the free memory)."""
+        self.wait()
+        self._hbm = None
 
     def fence(self):
         """Make the current compute stream wait (GPU-side) for the in-flight snapshot: with the HBM

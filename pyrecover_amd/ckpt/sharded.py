@@ -109,7 +109,8 @@ def save_ckpt_distributed(model, optimizer, lr_scheduler=None, sampler=None, ste
     if "sampler_state" in state:
         dstate["sampler"] = state["sampler_state"]
     dstate["pyrecover_state"] = {"rng": state["pyrecover_state"]["rng"],
-                                 "format": state["pyrecover_state"]["format"]}
+                                 "format": state["pyrecover_state"]["format"],
+                                 "reduction": state["pyrecover_state"]["reduction"]}
     if rngs is not None:
         dstate["pyrecover_state"]["rng_per_rank"] = {str(r): st for r, st in enumerate(rngs)}
     items = flatten_state(dstate)

@@ -27,9 +27,6 @@ from ..ops.reference import precompute_freqs_cis, rope_table
 from ..parallel.flat import FlatParams
 
 
-
-SHADOW_MIN_TOKENS = 0  # see Transformer.flatten_
-
 class RMSNorm(nn.Module):
     """Parameter container + reference-compatible eager forward (reference model.py:25-49)."""
 
@@ -206,17 +203,13 @@ class Transformer(nn.Module):
         Transposed weight shadows (K-contiguous W^T for the data-gradient GEMMs, rewritten by the
         optimizer): +3.5% at 7B B16 (profiles/ab_weight_shadows_s7.log), +5% at 7B B1 (99.1 vs
         104.1-104.4 ms), -0.5% at Llama-3-8B B1 (108.1 vs 107.6 ms; profiles/r4/shadow_policy_b1/),
-        so they are on from SHADOW_MIN_TOKENS (0) tokens per micro-step. PRA_WEIGHT_SHADOWS=1/0
-        forces them on/off; PRA_WEIGHT_SHADOWS_HEAD=0 leaves the output head without one."""
+        so they are on at every batch size. PRA_WEIGHT_SHADOWS=0 turns them off;
+        PRA_WEIGHT_SHADOWS_HEAD=0 leaves the output head without one."""
         if self.flat is None:
             self.flat = FlatParams(self.fusion_groups())
             # optimizer-state indices follow model.parameters() order, as in the reference
             self.flat.module_order = list(self.parameters())
-            env = os.environ.get("PRA_WEIGHT_SHADOWS", "")
-            if env in ("0", "1"):
-                shadows = env == "1"
-            else:
-                shadows = tokens_per_step is None or tokens_per_step >= SHADOW_MIN_TOKENS
+            shadows = os.environ.get("PRA_WEIGHT_SHADOWS", "1") != "0"
             head = os.environ.get("PRA_WEIGHT_SHADOWS_HEAD", "1") == "1"
             for mats in self._gemm_weights(head) if shadows else []:
                 self.flat.register_transposed(mats, (sum(p.shape[0] for p in mats), mats[0].shape[1]))

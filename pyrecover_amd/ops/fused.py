@@ -96,12 +96,30 @@ TN_WGRAD_WO = TN_WGRAD and os.environ.get("PYRECOVER_TN_WGRAD_WO", "1") == "1"
 # Shape limits of the HIP kernels (outside them the op runs the torch math of ops/reference.py on
 # the same device, like fp64): norms hold a row in registers (D <= 8192, 16-B chunks), embedding
 # rows and SwiGLU halves move as 16-B vectors.
+_FALLBACK_WARNED = set()
+
+
+def _note_fallback(op: str, t, ok: bool) -> bool:
+    """Warn once per (op, dtype, shape) when a GPU tensor leaves the HIP kernels for the torch
+    math of ops/reference.py (an unsupported head_dim, width or dtype): that path is correct
+    but can be many times slower (attention materialises the S x S scores)."""
+    if not ok and t.is_cuda:
+        key = (op, t.dtype, tuple(t.shape[-2:]))
+        if key not in _FALLBACK_WARNED:
+            _FALLBACK_WARNED.add(key)
+            import warnings
+
+            warnings.warn(f"pyrecover_amd: {op} on a {t.dtype} GPU tensor of shape {tuple(t.shape)} runs PyTorch "
+                          f"math (outside the HIP kernels' limits)", RuntimeWarning, stacklevel=3)
+    return ok
+
+
 def _norm_hip(x):
-    return _ext.hip(x) and x.shape[-1] % 8 == 0 and x.shape[-1] <= 8192
+    return _note_fallback("norm", x, _ext.hip(x) and x.shape[-1] % 8 == 0 and x.shape[-1] <= 8192)
 
 
 def _vec_hip(t, width):
-    return _ext.hip(t) and width % 8 == 0
+    return _note_fallback("elementwise", t, _ext.hip(t) and width % 8 == 0)
 
 
 def _tn_ok(t):
@@ -414,8 +432,8 @@ def add_layer_norm(x, delta, weight, bias, slot, eps):
 def _attn_hip(q, k):
     """The MFMA kernels: bf16/fp16 (attention.hip) or fp32 (attention_f32.hip, f32-input MFMA),
     head_dim 64 or 128, whole GQA groups, 16-B aligned rows."""
-    return (_ext.hip(q) and q.shape[-1] in (64, 128) and q.shape[2] % k.shape[2] == 0
-            and all(t.stride(-1) == 1 and t.stride(1) % 8 == 0 for t in (q, k)))
+    return _note_fallback("attention", q, _ext.hip(q) and q.shape[-1] in (64, 128) and q.shape[2] % k.shape[2] == 0
+                          and all(t.stride(-1) == 1 and t.stride(1) % 8 == 0 for t in (q, k)))
 
 
 def _attn_fwd(q, k, v, scale, causal):

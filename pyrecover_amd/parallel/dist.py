@@ -108,6 +108,54 @@ def rccl_pg_options():
     return opts
 
 
+# Reduction-order settings of RCCL: the algorithm, protocol and channel count decide how a bucket
+# is split and in which order each element's W contributions are added, so two runs (or a run and
+# its resumption after a requeue) reduce identically only when these match. RCCL's tuner picks them
+# per message size and topology unless they are set.
+RCCL_ORDER_KEYS = ("NCCL_ALGO", "NCCL_PROTO", "NCCL_MIN_NCHANNELS", "NCCL_MAX_NCHANNELS", "NCCL_NCHANNELS_PER_NET_PEER",
+                   "RCCL_MSCCL_ENABLE", "RCCL_MSCCLPP_ENABLE", "NCCL_IB_DISABLE", "NCCL_P2P_DISABLE")
+# What PYRECOVER_RCCL_DETERMINISTIC=1 pins (only keys the user left unset): ring all-reduce with the
+# Simple protocol over a fixed channel count, no MSCCL/MSCCL++ algorithm substitution. The ring
+# visits ranks in a fixed order, so every element is summed in the same order on every step.
+RCCL_PINNED = {"NCCL_ALGO": "Ring", "NCCL_PROTO": "Simple", "NCCL_MIN_NCHANNELS": "16", "NCCL_MAX_NCHANNELS": "16",
+               "RCCL_MSCCL_ENABLE": "0", "RCCL_MSCCLPP_ENABLE": "0"}
+
+
+def pin_rccl_order(environ=None) -> dict:
+    """With PYRECOVER_RCCL_DETERMINISTIC=1, set RCCL_PINNED's keys the environment leaves unset (before
+    the process group exists). Returns what was set."""
+    env = os.environ if environ is None else environ
+    if env.get("PYRECOVER_RCCL_DETERMINISTIC", "0") != "1":
+        return {}
+    done = {}
+    for k, v in RCCL_PINNED.items():
+        if k not in env:
+            env[k] = v
+            done[k] = v
+    return done
+
+
+def rccl_order_settings(environ=None) -> dict:
+    """The reduction-order settings in effect (recorded in every checkpoint's pyrecover_state)."""
+    env = os.environ if environ is None else environ
+    out = {k: env[k] for k in RCCL_ORDER_KEYS if k in env}
+    out["world_size"] = get_world_size() if _STATE.get("initialized") else 1
+    out["backend"] = _STATE.get("backend") or "none"
+    return out
+
+
+def compare_rccl_order(saved: Optional[dict], current: Optional[dict] = None) -> list:
+    """Differences between a checkpoint's recorded reduction settings and this run's (empty when
+    they match or nothing was recorded). A difference means the resumed run is not guaranteed to
+    reduce gradients in the same order as the run that wrote the checkpoint."""
+    if not saved:
+        return []
+    cur = rccl_order_settings() if current is None else current
+    keys = sorted(set(saved) | set(cur))
+    return [f"{k}: saved {saved.get(k, '<unset>')!r}, now {cur.get(k, '<unset>')!r}" for k in keys
+            if saved.get(k) != cur.get(k)]
+
+
 def maybe_init_distributed(activate_distributed: bool, backend: Optional[str] = None,
                            timeout_s: float = 1800.0) -> Tuple[int, int]:
     """Returns (local_rank, world_size). Initializes the process group when a multi-process
@@ -134,6 +182,9 @@ def maybe_init_distributed(activate_distributed: bool, backend: Optional[str] = 
     if not torch.distributed.is_initialized():
         kw = {}
         if backend == "nccl":
+            pinned = pin_rccl_order()
+            if pinned:
+                log_rank0(f"PYRECOVER_RCCL_DETERMINISTIC=1: pinned {pinned}")
             kw["device_id"] = torch.device("cuda", dev_index)
             opts = rccl_pg_options()
             if opts is not None:

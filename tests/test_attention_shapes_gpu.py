@@ -126,3 +126,19 @@ def test_flash_attention_op_fp32_hip_and_fp64_torch(cuda):
         assert _rel(o.double(), ref) < tol
         for got, want in ((q.grad, qd.grad), (k.grad, kd.grad), (v.grad, vd.grad)):
             assert _rel(got.double(), want) < 10 * tol
+
+
+def test_unsupported_head_dim_warns_once_and_stays_correct(cuda):
+    """head_dim 96 is outside the MFMA kernels: the op runs torch math on the GPU, warns once (not
+    silently 10x slower), and matches the oracle."""
+    F._FALLBACK_WARNED.clear()
+    q, k, v = _qkv(cuda, 1, 256, 4, 4, 96, torch.bfloat16)
+    with pytest.warns(RuntimeWarning, match="attention .* runs PyTorch math"):
+        o, _ = F._attn_fwd(q, k, v, 96 ** -0.5, True)
+    import warnings
+
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        F._attn_fwd(q, k, v, 96 ** -0.5, True)  # the second call is silent
+    ref_o = R.attention_ref(q.float(), k.float(), v.float(), True, 96 ** -0.5)
+    assert _rel(o, ref_o) < 1e-2

@@ -527,3 +527,28 @@ def test_trainer_grad_accumulation_and_checkpointing_run(tmp_path):
     assert r["step"] == 2
     r = _tiny_run(tmp_path, 4, ["--grad-accumulation-steps", "2", "--resume-from-checkpoint", "latest"])
     assert r["step"] == 4
+
+
+def test_reduction_settings_recorded_pinned_and_compared(tmp_path, caplog, monkeypatch):
+    """SURVEY §5.8 determinism contract: every checkpoint records the gradient-reduction settings
+    (world size, backend, RCCL algorithm / protocol / channels); a resume under different ones warns;
+    PYRECOVER_RCCL_DETERMINISTIC=1 pins ring / Simple / 16 channels where the user set nothing."""
+    import logging
+
+    from pyrecover_amd.ckpt import core as ckcore
+    from pyrecover_amd.parallel import dist as D
+
+    env = {"PYRECOVER_RCCL_DETERMINISTIC": "1", "NCCL_PROTO": "LL128"}
+    pinned = D.pin_rccl_order(env)
+    assert env["NCCL_ALGO"] == "Ring" and env["NCCL_PROTO"] == "LL128" and "NCCL_PROTO" not in pinned
+    assert env["NCCL_MIN_NCHANNELS"] == env["NCCL_MAX_NCHANNELS"] == "16"
+    assert D.pin_rccl_order({}) == {}
+    _tiny_run(tmp_path, 2)
+    ck = torch.load(tmp_path / "default-exp" / "ckpt_2.pt", weights_only=True)
+    red = ck["pyrecover_state"]["reduction"]
+    assert red["world_size"] == 1 and "backend" in red
+    assert ckcore.warn_reduction_change(ck["pyrecover_state"]) == []
+    monkeypatch.setenv("NCCL_ALGO", "Tree")
+    with caplog.at_level(logging.WARNING, logger="pyrecover"):
+        diffs = ckcore.warn_reduction_change(ck["pyrecover_state"])
+    assert diffs and "NCCL_ALGO" in diffs[0] and "gradient-reduction" in caplog.text
