@@ -40,6 +40,9 @@
 #ifndef PRA_FWD_PRESCALE
 #define PRA_FWD_PRESCALE 0
 #endif
+#ifndef PRA_DQ_PRESCALE
+#define PRA_DQ_PRESCALE 0
+#endif
 
 namespace pra {
 namespace attn {
@@ -914,6 +917,162 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
 }
 
 // ======================================================================================
+// Backward dK/dV, ring-staged (NW = 8, S % 256 == 0): the bwd_dkdv_kernel<.., 8, .., KREG> math with
+//  * K of the wave's 32 keys loaded straight from global memory into registers (pre-multiplied by
+//    scale log2(e) there), so K takes no LDS and its 8 row reads per query tile are gone;
+//  * V of the block resident in LDS (LDS-DMA), read as the dP chain's row operand;
+//  * Q / dO tiles and their row constants (-lse log2(e), -delta: the dQ kernel's RC2 output) moved by
+//    LDS-DMA into a double buffer one tile ahead: no VGPR staging, no ds_write, and ONE barrier per
+//    32-query tile instead of two.
+// LDS: 64 KB (V) + 2 x 16.25 KB at D = 128.
+// ======================================================================================
+template <typename T, int D, bool CAUSAL>
+__global__ __launch_bounds__(512, 1) void bwd_dkdv_r_kernel(
+    const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V, const T* __restrict__ dO,
+    const float* __restrict__ RC, long nrc, T* __restrict__ dK, T* __restrict__ dV, int S, int Hq, int Hkv,
+    long ldq, long ldk, long ldv, long lddo, long lddk, long lddv, float scale, float scale_log2, int skv,
+    const float2* __restrict__ rtab) {
+  constexpr int NW = 8, KB = 32 * NW, QT = 32;
+  constexpr int NKS = D / 16, NDB = D / 32;
+  constexpr int KVT = KB * D, QDT = QT * D;
+  __shared__ __attribute__((aligned(16))) T Vs[KVT];
+  // per buffer: Q | dO tiles, then 64 floats: -lse log2(e) [32] | -delta [32] (one object per buffer:
+  // separate alias scopes, so reads of one buffer do not wait for the DMA filling the other)
+  __shared__ __attribute__((aligned(16))) T qd0[2 * QDT];
+  __shared__ __attribute__((aligned(16))) T qd1[2 * QDT];
+  __shared__ __attribute__((aligned(16))) float rc0[64];
+  __shared__ __attribute__((aligned(16))) float rc1[64];
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h2 = lane >> 5, l32 = lane & 31;
+  const int nkb = S / KB;
+  const int BH = gridDim.x / nkb;
+  const int kbk = (int)(blockIdx.x / BH);  // causal: early key tiles have the most work
+  const int bh = blockIdx.x % BH;
+  const int hk = bh % Hkv, b = bh / Hkv;
+  const int nrep = Hq / Hkv;
+  const int k0 = kbk * KB, kw = k0 + wid * 32;
+  const int krow = kw + l32;
+
+  GStage<T, D, KB, NW> gv;
+  gv.init(ldv);
+  gv.issue(V + ((long)b * S + k0) * ldv + hk * D, Vs);
+  GStage<T, D, QT, NW> gq, gd;
+  gq.init(ldq);
+  gd.init(lddo);
+  const T* Kw = nullptr;
+  (void)Kw;
+  const T* Vw = Vs + wid * 32 * D;
+  LaneOff<T, D> lo;
+  lo.init(lane);
+
+  // the wave's K rows as the S chain's B operand: lane holds K[krow][16 ks + 8 h2 .. + 7] * c
+  V8<T> kf[NKS];
+  {
+    const T* kr = K + ((long)b * S + krow) * ldk + hk * D + 8 * h2;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      kf[ks] = *reinterpret_cast<const V8<T>*>(kr + 16 * ks);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) kf[ks][j] = (T)((float)kf[ks][j] * scale_log2);
+    }
+  }
+
+  f32x16 dkt[NDB], dvt[NDB];
+#pragma unroll
+  for (int i = 0; i < NDB; ++i) { dkt[i] = f32x16{}; dvt[i] = f32x16{}; }
+
+  const int qstart = CAUSAL ? k0 : 0;
+  const int nqt = (S - qstart) / QT;
+  const int total = nqt * nrep;
+  const long rc_b = (long)b * Hq * S;
+  auto issue = [&](int it, T* qd, float* rc) {
+    const int hq = hk * nrep + it / nqt;
+    const int q0 = qstart + (it % nqt) * QT;
+    gq.issue(Q + ((long)b * S + q0) * ldq + hq * D, qd);
+    gd.issue(dO + ((long)b * S + q0) * lddo + hq * D, qd + QDT);
+    if (wid == 0 && lane < 16) {  // 2 x 128 B of row constants: lanes 0-7 -lse log2(e), 8-15 -delta
+      const float* src = RC + (lane < 8 ? 0 : nrc) + rc_b + (long)hq * S + q0 + 4 * (lane & 7);
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)rc, 16, 0, 0);
+    }
+  };
+  if (total > 0) issue(0, qd0, rc0);
+  __syncthreads();  // V and tile 0 landed (vmcnt(0) before the barrier)
+
+  auto body = [&](auto cc, int it) {
+    constexpr int CUR = decltype(cc)::value;
+    T* const qd = CUR ? qd1 : qd0;
+    const float* rc = CUR ? rc1 : rc0;
+    if (it + 1 < total) issue(it + 1, CUR ? qd0 : qd1, CUR ? rc0 : rc1);
+    const T* Qs = qd;
+    const T* Ds = qd + QDT;
+    const int q0 = qstart + (it % nqt) * QT;
+    if (!(CAUSAL && q0 + QT - 1 < kw)) {
+      const bool diag = CAUSAL && q0 == kw;
+      // S' = (c K) Q^T - lse log2(e), dP' = dO V^T - delta: the accumulators start at the row
+      // constants of their query rows crow(r, h2); the causal mask rides on S's initial values
+      f32x16 sa, dp;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const float4 a = *reinterpret_cast<const float4*>(rc + 8 * rr + 4 * h2);
+        const float4 c = *reinterpret_cast<const float4*>(rc + 32 + 8 * rr + 4 * h2);
+        sa[4 * rr] = a.x; sa[4 * rr + 1] = a.y; sa[4 * rr + 2] = a.z; sa[4 * rr + 3] = a.w;
+        dp[4 * rr] = c.x; dp[4 * rr + 1] = c.y; dp[4 * rr + 2] = c.z; dp[4 * rr + 3] = c.w;
+      }
+      if (diag) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (l32 > crow(r, h2)) sa[r] = -INFINITY;
+      }
+      V8<T> xa = lo.rowk(Qs, 0, 0), xb = kf[0];
+#pragma unroll
+      for (int st = 0; st < 2 * NKS; ++st) {
+        const int ks = st % NKS;
+        V8<T> na = xa, nb = xb;
+        if (st + 1 < 2 * NKS) {
+          const int nks = (st + 1) % NKS;
+          na = lo.rowk(st + 1 < NKS ? Qs : Ds, 0, nks);
+          nb = st + 1 < NKS ? kf[nks] : lo.rowk(Vw, 0, nks);
+        }
+        if (st < NKS) sa = mfma(xa, xb, sa);
+        else dp = mfma(xa, xb, dp);
+        xa = na; xb = nb;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float p = fexp2(sa[r]);
+        if (!CAUSAL && krow >= skv) p = 0.f;  // padded key
+        sa[r] = p;
+        dp[r] = p * dp[r];
+      }
+      const V8<T> p0 = pack8<T>(sa, 0), p1 = pack8<T>(sa, 1), d0 = pack8<T>(dp, 0), d1 = pack8<T>(dp, 1);
+      V8<T> ot = lo.tr(Ds, 0, 0), qt = lo.tr(Qs, 0, 0);
+#pragma unroll
+      for (int st = 0; st < 2 * NDB; ++st) {
+        const int s2 = st / NDB, db = st % NDB;
+        V8<T> no = ot, nq = qt;
+        if (st + 1 < 2 * NDB) {
+          no = lo.tr(Ds, 16 * ((st + 1) / NDB), (st + 1) % NDB);
+          nq = lo.tr(Qs, 16 * ((st + 1) / NDB), (st + 1) % NDB);
+        }
+        dvt[db] = mfma(ot, s2 ? p1 : p0, dvt[db]);
+        dkt[db] = mfma(qt, s2 ? d1 : d0, dkt[db]);
+        ot = no; qt = nq;
+      }
+    }
+    __syncthreads();  // tile it + 1 landed; this buffer is free for tile it + 2
+  };
+  for (int it = 0; it < total; it += 2) {
+    body(IC<0>{}, it);
+    if (it + 1 < total) body(IC<1>{}, it + 1);
+  }
+
+  store_rows16<T, NDB>(dkt, scale, dK + ((long)b * S + krow) * lddk + hk * D, true, h2,
+                       rtab ? rtab + (long)min(krow, skv - 1) * (D / 2) : nullptr);
+  store_rows16<T, NDB>(dvt, 1.f, dV + ((long)b * S + krow) * lddv + hk * D, true, h2);
+}
+
+// ======================================================================================
 // Backward dK/dV, one wave per SIMD, two query sub-tiles in flight: block = (b, kv head, 128
 // keys), 4 waves x 32 keys; each step stages 64 queries (sub-tiles A and B of 32). With the whole
 // 512-entry register file per wave, a wave keeps S/dP of both sub-tiles live and runs them as a
@@ -1210,6 +1369,16 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
       }
     }
     dl = half_sum(part);  // all 64 lanes (permlane32 swap)
+#if PRA_DQ_PRESCALE
+    // PIPE path: Q pre-multiplied by scale log2(e) (as the forward's PRA_FWD_PRESCALE), and the S / dP
+    // accumulators start at -lse log2(e) / -delta, so p = exp2(S') and dS = p dP' need no FMA / sub
+    if (PIPE) {
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[ks][j] = (T)((float)qf[ks][j] * scale_log2);
+    }
+#endif
     if (qrow < S && h2 == 0) {
       const long i = ((long)b * Hq + hq) * S + qrow;
       Delta[i] = dl;
@@ -1251,7 +1420,23 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
         constexpr int R1 = NKS, R3 = NDB, NR = 2 * R1 + 2 * R3;
         constexpr int EA = 16 / R1, EB = 16 / R3;
         const int lim = qrow - k0 - 4 * h2;
+#if PRA_DQ_PRESCALE == 1
+        f32x16 s0, s1, p0, p1;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          s0[r] = -lse2;
+          p0[r] = -dl;
+        }
+        s1 = s0;
+        p1 = p0;
+#elif PRA_DQ_PRESCALE == 2  // S chains only (16 registers of constants instead of 32)
+        f32x16 s0, s1, p0 = f32x16{}, p1 = f32x16{};
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s0[r] = -lse2;
+        s1 = s0;
+#else
         f32x16 s0 = f32x16{}, s1 = f32x16{}, p0 = f32x16{}, p1 = f32x16{};
+#endif
         V8<T> g0[2], g1[2];
         auto fetch = [&](int k, V8<T> (&o)[4]) {
           if (k < 2 * R1) {
@@ -1266,9 +1451,19 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
           }
         };
         auto soft = [&](f32x16& sv, f32x16& dp, int kb, int r) {
+#if PRA_DQ_PRESCALE == 1
+          float p = fexp2(sv[r]);
+          if (MASK && crow(r, 0) > lim - 32 * kb) p = 0.f;
+          dp[r] = p * dp[r];
+#elif PRA_DQ_PRESCALE == 2
+          float p = fexp2(sv[r]);
+          if (MASK && crow(r, 0) > lim - 32 * kb) p = 0.f;
+          dp[r] = p * (dp[r] - dl);
+#else
           float p = fexp2(fmaf(sv[r], scale_log2, -lse2));
           if (MASK && crow(r, 0) > lim - 32 * kb) p = 0.f;
           dp[r] = p * (dp[r] - dl);
+#endif
         };
         V8<T> cur[4], nxt[4];
         fetch(0, cur);
@@ -1384,11 +1579,13 @@ struct AttnOptions {
   // the overlapped optimizer, and its fp32 partial sums would make the gradients depend on whether
   // the optimizer overlaps (tests/test_xgmi_gpu.py compares the two bitwise)
   int dkdv_split = 1;
-  // two-wave dK/dV kernel (NW = 8, D = 128): 1 = K fragments held in registers (KREG), 0 = read from
-  // LDS (default), -1 = KREG unless a side-stream job waits for the dK/dV window (below)
-  // (B16 S2048 H32 bwd 2.387 -> 2.358 ms alone, but 1058.0 vs 1055.5 ms in the 7B step:
+  // two-wave dK/dV kernel (NW = 8, D = 128): 2 = ring-staged bwd_dkdv_r_kernel (default: K in
+  // registers, Q/dO by LDS-DMA, one barrier per query tile; B16 S2048 H32 bwd 2.39 -> 2.27 ms,
+  // profiles/r5/attn/harness_dkdv_ring.log), 1 = bwd_dkdv_kernel with K fragments held in registers
+  // (KREG), 0 = bwd_dkdv_kernel reading K from LDS, -1 = KREG unless a side-stream job waits for the
+  // dK/dV window (below) (r4: KREG 2.387 -> 2.358 ms alone, but 1058.0 vs 1055.5 ms in the 7B step:
   // profiles/r4/attn_ab_dkdv_kreg_b16.log, step_ab_7b_b16_kreg.log)
-  int dkdv_kreg = 0;
+  int dkdv_kreg = 2;
 };
 AttnOptions g_attn_opts;
 
@@ -1482,7 +1679,8 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
   // (-lse log2(e), -delta), written by the dQ kernel only when that kernel runs
   const long nrc = (long)B * Hq * S;
   const bool p2 = dkdv_use_p2(B, S, Hq, Hkv, D);
-  float* rc2 = p2 ? delta + nrc : nullptr;
+  const bool ring = g_attn_opts.dkdv_kreg == 2 && !p2 && nw == 8 && D == 128;  // bwd_dkdv_r_kernel
+  float* rc2 = (p2 || ring) ? delta + nrc : nullptr;
   // dQ first: it also computes delta = rowsum(dO * O), which the dK/dV kernel reads
   {
     dim3 grid((S / (32 * nw)) * Hq * B);
@@ -1524,6 +1722,14 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
       hipLaunchKernelGGL((dkdv_reduce_kernel<T>), dim3((unsigned)((2 * n / 4 + 255) / 256)), dim3(256), 0, st,
                          (const float*)part, ns, n, Hkv * D, (T*)dk, lddk, (T*)dv, lddv);
     }
+  } else if (ring) {
+    dim3 grid((S / 256) * Hkv * B);
+#define LAUNCHR(DD, CC)                                                                                       \
+  hipLaunchKernelGGL((bwd_dkdv_r_kernel<T, DD, CC>), grid, dim3(512), 0, st, (const T*)q, (const T*)k,        \
+                     (const T*)v, (const T*)dout, rc2, nrc, (T*)dk, (T*)dv, S, Hq, Hkv, ldq, ldk, ldv, lddo,   \
+                     lddk, lddv, scale, sl2, skv, rt)
+    if (causal) LAUNCHR(128, true); else LAUNCHR(128, false);
+#undef LAUNCHR
   } else {
     dim3 grid((S / (32 * nw)) * Hkv * B);
 #define LAUNCH(DD, CC, NWW, ...)                                                                                \

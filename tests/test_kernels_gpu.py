@@ -255,15 +255,18 @@ def test_attention_bwd(cuda, B, S, Hq, Hkv, D, causal):
     assert torch.equal(dqkv, dqkv2)
 
 
-@pytest.mark.parametrize("impl", [0, 1, 2])
+@pytest.mark.parametrize("impl", [0, 1, 2, 3])
 @pytest.mark.parametrize("B,S,Hq,Hkv,D,causal", [(1, 1024, 4, 1, 128, True), (2, 512, 4, 2, 128, False),
                                                  (1, 640, 2, 2, 64, True)])
 def test_attention_bwd_dkdv_kernels(cuda, attn_opts, impl, B, S, Hq, Hkv, D, causal):
-    """Both backward kernel generations -- dK/dV two-wave vs one-wave-per-SIMD pipelined
+    """Every backward kernel generation -- dK/dV two-wave vs one-wave-per-SIMD pipelined
     (dkdv_impl), dQ plain vs region-pipelined (dq_pipe) -- against the fp32 oracle, with
     multi-step loops, GQA and the causal diagonal. impl 2: the two-wave kernel with K held in
-    registers (dkdv_kreg; 256-key blocks at D = 128)."""
-    attn_opts(dkdv_impl=min(impl, 1) if impl < 2 else 0, dq_pipe=min(impl, 1), dkdv_kreg=int(impl == 2))
+    registers (dkdv_kreg 1; 256-key blocks at D = 128); impl 3: the ring-staged two-wave kernel
+    (dkdv_kreg 2, the default: K in registers, Q/dO/row constants by LDS-DMA), bitwise equal to the
+    LDS-K kernel."""
+    kreg = {0: 0, 1: 0, 2: 1, 3: 2}[impl]
+    attn_opts(dkdv_impl=min(impl, 1) if impl < 2 else 0, dq_pipe=min(impl, 1), dkdv_kreg=kreg)
     C = _ext.native()
     _, q, k, v = _qkv(cuda, B, S, Hq, Hkv, D, seed=5)
     scale = 1 / math.sqrt(D)
@@ -279,7 +282,7 @@ def test_attention_bwd_dkdv_kernels(cuda, attn_opts, impl, B, S, Hq, Hkv, D, cau
     dq2, dk2, dv2 = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
     C.attn_bwd(q, k, v, o, do, lse, dq2, dk2, dv2, scale, causal)
     assert torch.equal(dq, dq2) and torch.equal(dk, dk2) and torch.equal(dv, dv2)
-    if impl == 2:  # K in registers reads the same values as K from LDS: bitwise the same gradients
+    if impl >= 2:  # K in registers reads the same values as K from LDS: bitwise the same gradients
         attn_opts(dkdv_kreg=0)
         C.attn_bwd(q, k, v, o, do, lse, dq2, dk2, dv2, scale, causal)
         assert torch.equal(dq, dq2) and torch.equal(dk, dk2) and torch.equal(dv, dv2)
