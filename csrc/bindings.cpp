@@ -779,6 +779,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("grad_norm", &grad_norm);
   m.def("wgrad_mm_", &wgrad_mm_);
   m.def("wgrad_mm_exp_", &wgrad_mm_exp_);
+  m.def("wgrad_set_streamk", &pra_wgrad_set_streamk,
+        "weight-gradient schedule: 0 whole tiles + split tail, 1 stream-K when tiles % CUs != 0, 2 always");
+  m.def("wgrad_get_streamk", &pra_wgrad_get_streamk);
   m.def("gemm_nt_", &gemm_nt_, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("epi") = 0,
         py::arg("out2") = py::none(), py::arg("tab") = py::none(), py::arg("S") = 0, py::arg("D") = 0,
         py::arg("nrot") = 0);

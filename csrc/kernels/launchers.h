@@ -44,6 +44,10 @@ hipError_t pra_wgrad_gemm_exp(const void* A, const void* B, void* C, int M, int 
                               long ldc, int exp, hipStream_t s);
 long pra_wgrad_ws_floats(int M, int N, int K, int cus);
 int pra_wgrad_ticket_count(int M, int N, int K, int cus);
+// weight-gradient tile schedule: 0 = whole tiles + split partial last round, 1 = stream-K where the
+// tile count is not a multiple of the CU count, 2 = stream-K always (gemm_wgrad.hip)
+void pra_wgrad_set_streamk(int mode);
+int pra_wgrad_get_streamk();
 // C = A B^T, A [M][K], B [N][K] (both K-contiguous) with a fused epilogue (gemm_nt.hip):
 // epi 0 plain, 1 SwiGLU forward (C = gu [M][2F], c2 = a [M][F]), 2 SwiGLU backward in place over
 // gu (C), 3 RoPE on the first nrot columns (tab float2 [S][D/2])

@@ -587,3 +587,40 @@ def test_wgrad_mm_split_tail_under_hip_graph_capture(cuda):
         assert torch.equal(out, ref)
     exact = a.float().t() @ b.float()
     assert ((out.float() - exact).norm() / exact.norm()).item() < 5e-3
+
+
+@pytest.fixture
+def wgrad_streamk():
+    C_ = _ext.native()
+    prev = C_.wgrad_get_streamk()
+    yield C_.wgrad_set_streamk
+    C_.wgrad_set_streamk(prev)
+
+
+@pytest.mark.parametrize("K,M,N", [(2048, 6144, 4096), (1024, 7680, 2560), (96, 1280, 256), (64, 256, 256),
+                                   (4096, 4096, 14336)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_wgrad_mm_streamk_vs_fp32(cuda, wgrad_streamk, K, M, N, accumulate):
+    """The stream-K schedule (one workgroup per CU, each an equal share of the tile x k-step
+    iterations; tiles covered by several workgroups summed from fp32 partials in k order by the last
+    arriver): against an fp64 oracle, with accumulate, bit-identical run to run -- including ranges
+    shorter than one tile (few tiles, short K) -- and within rounding of the default schedule."""
+    C_ = _ext.native()
+    g = torch.Generator(device=cuda)
+    g.manual_seed(K + M + N)
+    a = torch.randn(K, M, device=cuda, generator=g).bfloat16()
+    b = torch.randn(K, N, device=cuda, generator=g).bfloat16()
+    c0 = torch.randn(M, N, device=cuda, generator=g).bfloat16()
+    wgrad_streamk(2)
+    out = c0.clone()
+    C_.wgrad_mm_(a, b, out, accumulate)
+    ref = a.double().t() @ b.double() + (c0.double() if accumulate else 0)
+    err = ((out.double() - ref).abs() / (ref.abs() + math.sqrt(K))).max().item()
+    assert err < 1e-2, err
+    out2 = c0.clone()
+    C_.wgrad_mm_(a, b, out2, accumulate)
+    assert torch.equal(out, out2)  # deterministic
+    wgrad_streamk(0)
+    out3 = c0.clone()
+    C_.wgrad_mm_(a, b, out3, accumulate)
+    assert ((out3.float() - out.float()).abs() <= out.float().abs() * 2 ** -7 + 1e-2).all().item()
