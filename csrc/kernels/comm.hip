@@ -1,8 +1,9 @@
 // Reduction kernel of the intra-node xGMI all-reduce (csrc/dist/xgmi.cpp, pyrecover_amd/parallel/
 // xgmi.py): dst = src_0 + src_1 + ... + src_{W-1}, summed in fp32 in rank order and rounded
 // once, so every rank reduces its slice identically (bit-reproducible, unlike a ring that rounds
-// at every hop). The sources are this rank's own slice and the peers' slices already copied into
-// local staging by the copy engines.
+// at every hop). The sources are this rank's own slice and the peers' slices, read straight from
+// their IPC-mapped gradient buffers over xGMI (the pull reduce-scatter of XgmiEngine), or copies of
+// them in local staging (the copy-engine path).
 #include "common.h"
 
 namespace pra {
@@ -90,5 +91,57 @@ extern "C" hipError_t pra_copy_d2d(void* dst, const void* src, long nbytes, hipS
   if (tail > 0)
     hipLaunchKernelGGL(pra::copy1_kernel, dim3((tail + 255) / 256), dim3(256), 0, s,
                        (unsigned char*)dst + n16 * 16, (const unsigned char*)src + n16 * 16, tail);
+  return hipGetLastError();
+}
+
+// All-gather phase of the pull all-reduce (csrc/dist/xgmi.cpp XgmiEngine): every peer's reduced
+// slice is pulled from its IPC-mapped buffer into this rank's buffer in ONE kernel, the W - 1 source
+// GPUs spread over blockIdx.y, so the pulls from all peers (all xGMI links) run at once. Slices are
+// 16-B aligned (8-element cuts); a tail of n % 16 bytes is copied bytewise by the last block row.
+namespace pra {
+struct CopyList {
+  const void* src[16];
+  void* dst[16];
+  long nbytes[16];
+};
+__global__ __launch_bounds__(256) void pull_gather_kernel(CopyList l) {
+  const int k = blockIdx.y;
+  const long n16 = l.nbytes[k] / 16;
+  const uint4* __restrict__ src = reinterpret_cast<const uint4*>(l.src[k]);
+  uint4* __restrict__ dst = reinterpret_cast<uint4*>(l.dst[k]);
+  const long stride = (long)gridDim.x * 256;
+  long i = (long)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    dst[i] = a;
+    dst[i + stride] = b;
+    dst[i + 2 * stride] = c;
+    dst[i + 3 * stride] = d;
+  }
+  for (; i < n16; i += stride) dst[i] = src[i];
+  const long tail = l.nbytes[k] - n16 * 16;
+  if (blockIdx.x == 0 && threadIdx.x < tail)
+    reinterpret_cast<unsigned char*>(l.dst[k])[n16 * 16 + threadIdx.x] =
+        reinterpret_cast<const unsigned char*>(l.src[k])[n16 * 16 + threadIdx.x];
+}
+}  // namespace pra
+
+extern "C" hipError_t pra_pull_gather(const void* const* srcs, void* const* dsts, const long* nbytes, int n,
+                                      hipStream_t s) {
+  if (n < 0 || n > 16) return hipErrorInvalidValue;
+  if (n == 0) return hipSuccess;
+  pra::CopyList l{};
+  long mx = 0;
+  for (int k = 0; k < n; ++k) {
+    if (reinterpret_cast<uintptr_t>(srcs[k]) % 16 || reinterpret_cast<uintptr_t>(dsts[k]) % 16) return hipErrorInvalidValue;
+    l.src[k] = srcs[k];
+    l.dst[k] = dsts[k];
+    l.nbytes[k] = nbytes[k];
+    mx = nbytes[k] > mx ? nbytes[k] : mx;
+  }
+  long bx = (mx / 16 + 1023) / 1024;  // ~4 x 16 B per thread per pass
+  if (bx > 512) bx = 512;
+  if (bx < 1) bx = 1;
+  hipLaunchKernelGGL(pra::pull_gather_kernel, dim3((unsigned)bx, (unsigned)n), dim3(256), 0, s, l);
   return hipGetLastError();
 }

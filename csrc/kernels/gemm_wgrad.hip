@@ -329,10 +329,15 @@ __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, c
         store_c(m0, n0);
       } else {
         put_partial(2L * g + (t == first_tile ? 0 : 1));
+        // the ranges on this tile: the non-empty ones between the owners of its first and last
+        // iteration (with fewer iterations than workgroups, empty ranges sit in between)
         const int glo = owner((long)t * nk), ghi = owner((long)(t + 1) * nk - 1);
-        if (arrive(tickets + t, ghi - glo + 1)) {
+        int nseg = 0;
+        for (int gg = glo; gg <= ghi; ++gg) nseg += start(gg + 1) > start(gg);
+        if (arrive(tickets + t, nseg)) {
           zero_acc();
           for (int gg = glo; gg <= ghi; ++gg) {
+            if (start(gg + 1) <= start(gg)) continue;
             const bool gfirst = (int)(start(gg) / nk) == t;
             add_partial(2L * gg + (gfirst ? 0 : 1));
           }

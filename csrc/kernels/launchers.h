@@ -72,6 +72,8 @@ hipError_t pra_grad_norm(int dtype, const void* x, long n, float* ws, float* out
 // dst <- src, nbytes, device memory (16-B vector path when both are 16-B aligned)
 hipError_t pra_copy_d2d(void* dst, const void* src, long nbytes, hipStream_t s);
 hipError_t pra_sum_slices(int dtype, const void* const* srcs, int nsrc, void* dst, long n, hipStream_t s);
+// n (<= 16) copies src[k] -> dst[k] of nbytes[k] in one kernel (16-B aligned pointers)
+hipError_t pra_pull_gather(const void* const* srcs, void* const* dsts, const long* nbytes, int n, hipStream_t s);
 
 hipError_t pra_adamw_t(int dtype, void* p, const void* g, void* m, void* v, void* pt, int rows, int cols, double lr,
                        double b1, double b2, double eps, double wd, double bc1, double bc2_sqrt, float gscale,

@@ -2,22 +2,26 @@
 
 RCCL's ring moves every byte around the 8 GPUs over one link per direction per ring. On an MI355X
 node every GPU has a direct xGMI link to each of its 7 peers, so this backend works per link
-instead:
+instead. Default engine (``csrc/dist/xgmi.cpp`` XgmiEngine, native):
 
-* reduce-scatter: rank r owns slice r of each bucket and pulls that slice from all peers at once,
-  one copy per peer on its own HIP stream, so all 7 links are busy;
-* a rank-ordered fp32 reduction kernel (``sum_slices``) sums the slices. The order is fixed and
-  there is one rounding, so every rank gets bit-identical values, deterministically;
-* all-gather: every rank pulls the reduced slices back from their owners, again one stream per peer.
+* reduce-scatter: rank r owns slice r of each bucket; ONE pull-reduce kernel reads slice r from
+  every rank's IPC-mapped gradient buffer (the 7 peers' over their xGMI links at once) and sums them
+  in fp32 in rank order into its own buffer: one rounding, so every rank gets bit-identical values,
+  deterministically, and no staging copy;
+* all-gather: ONE pull-gather kernel copies every owner's reduced slice into this rank's buffer;
+* both kernels run on one high-priority comm stream, scheduled by a C++ worker thread, so the
+  backward thread only records an event and enqueues the bucket (no Python in the critical window,
+  one hardware queue for all of it).
 
-Per bucket, the traffic per link is bucket/W per phase.
+Per bucket, the traffic per link is bucket/W per phase. ``PYRECOVER_XGMI_ENGINE=copy`` selects the
+earlier copy-engine path (one copy stream per peer into local staging, then the reduction kernel,
+orchestrated by a Python thread).
 
-Cross-process ordering uses interprocess HIP events only. A peer's copy stream waits, on the GPU,
-on this rank's "bucket ready" / "slice reduced" events, and no kernel spins. The host only
+Cross-process ordering uses interprocess HIP events only: a rank's comm stream waits, on the GPU,
+on its peers' "bucket ready" / "slice reduced" events, and no kernel spins. The host only
 guarantees that an event was recorded (for THIS step) before anyone waits on it: every rank
 publishes a per-bucket sequence number in a page of host shared memory right after recording, and
-the comm thread of a peer polls that word (microseconds) instead of the two gloo barriers per
-bucket an earlier version paid (a TCP round trip each). The backward thread never blocks.
+the worker of a peer polls that word (microseconds). The backward thread never blocks.
 
 The gradient buffer is reallocated with ``hipMalloc`` so it can be exported with
 ``hipIpcGetMemHandle``. Opt-in: ``GradReducer(..., backend="xgmi")``, ``train.py --allreduce
@@ -25,6 +29,7 @@ xgmi``, ``bench.py --allreduce xgmi``. RCCL stays the default.
 """
 from __future__ import annotations
 
+import os
 import queue
 import threading
 import time
@@ -67,6 +72,9 @@ class _Work:
 
     def wait(self):
         """Current stream waits (GPU-side) for the all-reduced bucket."""
+        if self.owner.eng is not None:
+            self.owner.eng.wait(self.b, torch.cuda.current_stream(self.owner.dev).cuda_stream)
+            return
         self.ready.wait()
         if self.owner.error is not None:
             raise RuntimeError(f"xgmi all-reduce failed: {self.owner.error}")
@@ -117,6 +125,10 @@ class _HostSeq:
                 time.sleep(20e-6)  # releases the GIL for the backward thread
             if time.perf_counter() - t0 > timeout:
                 raise TimeoutError(f"xgmi: rank {r} did not publish slot {slot} seq {seq}")
+
+    def address(self) -> int:
+        """Base address of the [world, slots] int64 words in this process (for the native engine)."""
+        return self.a.ctypes.data
 
     def close(self):
         if getattr(self, "a", None) is None:
@@ -194,9 +206,6 @@ class XgmiAllReduce:
             n = hi - lo
             cuts = [lo + ((n * r // W) // 8) * 8 for r in range(W)] + [hi]
             self.slices.append([(cuts[r], cuts[r + 1]) for r in range(W)])
-        max_slice = max((s1 - s0) for sl in self.slices for s0, s1 in sl)
-        self.stride = ((max_slice + 63) // 64) * 64
-        self.staging = torch.empty(max(1, (W - 1) * self.stride), dtype=self.dtype, device=self.dev)
         # 5) events: per bucket "ready" and "reduced" (interprocess), one per-step "done"
         nb = len(self.ranges)
         self.ev_ready = [self.C.ipc_event_create(di) for _ in range(nb)]
@@ -216,33 +225,56 @@ class XgmiAllReduce:
                 self.peer_ready.append([self.C.ipc_event_open(h, di) for h in allh[r][0]])
                 self.peer_rs.append([self.C.ipc_event_open(h, di) for h in allh[r][1]])
                 self.peer_step.append(self.C.ipc_event_open(allh[r][2], di))
-        self.ev_done = [torch.cuda.Event() for _ in range(nb)]
-        self.ev_sum = torch.cuda.Event()
-        # 6) streams: one per peer (parallel links) + the reduction stream
-        self.comm = torch.cuda.Stream(device=self.dev)
-        self.copy = {r: torch.cuda.Stream(device=self.dev) for r in range(W) if r != self.rank}
-        # 7) host sequence words: [ready b | reduced b | step]
+        # 6) host sequence words: [ready b | reduced b | step]
         self.nb = nb
         self.seq = 1  # current step's sequence number (published values start at 1)
         self.hseq = _HostSeq(self.rank, W, 2 * nb + 1, self.hgroup)
-        # 8) comm thread
-        self.q: "queue.Queue" = queue.Queue()
         self.error = None
-        self.works: List[_Work] = []
-        self.th = threading.Thread(target=self._loop, name="pyrecover-xgmi", daemon=True)
-        self.th.start()
+        self.eng = None
+        if os.environ.get("PYRECOVER_XGMI_ENGINE", "pull") != "copy":
+            # default: the native engine (csrc/dist/xgmi.cpp XgmiEngine) -- one comm stream, one
+            # pull-reduce kernel reading every peer's slice over xGMI and one pull-gather kernel per
+            # bucket, scheduled by a C++ worker thread
+            code = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}[self.dtype]
+            cuts = [c for sl in self.slices for c in [s0 for s0, _ in sl] + [sl[-1][1]]]
+            self.eng = self.C.XgmiEngine(
+                di, self.rank, W, code, self.esz, list(self.peer_base), cuts, self.hseq.address(),
+                list(self.ev_ready), list(self.ev_rs), self.ev_step,
+                [e for r in range(W) for e in self.peer_ready[r]], [e for r in range(W) for e in self.peer_rs[r]],
+                list(self.peer_step))
+        else:
+            # copy-engine path: per-peer copy streams into local staging, the rank-ordered reduction
+            # on a comm stream, orchestrated by a Python thread
+            max_slice = max((s1 - s0) for sl in self.slices for s0, s1 in sl)
+            self.stride = ((max_slice + 63) // 64) * 64
+            self.staging = torch.empty(max(1, (W - 1) * self.stride), dtype=self.dtype, device=self.dev)
+            self.ev_done = [torch.cuda.Event() for _ in range(nb)]
+            self.ev_sum = torch.cuda.Event()
+            self.comm = torch.cuda.Stream(device=self.dev)
+            self.copy = {r: torch.cuda.Stream(device=self.dev) for r in range(W) if r != self.rank}
+            self.q: "queue.Queue" = queue.Queue()
+            self.works: List[_Work] = []
+            self.th = threading.Thread(target=self._loop, name="pyrecover-xgmi", daemon=True)
+            self.th.start()
         dist.barrier(group=self.hgroup)
 
     # --- backward thread -----------------------------------------------------------------
     def launch(self, b: int) -> _Work:
-        self.C.event_record(self.ev_ready[b], torch.cuda.current_stream(self.dev).cuda_stream)
         w = _Work(self, b)
+        if self.eng is not None:
+            self.eng.launch(b, torch.cuda.current_stream(self.dev).cuda_stream)
+            return w
+        self.C.event_record(self.ev_ready[b], torch.cuda.current_stream(self.dev).cuda_stream)
         self.q.put((b, w))
         return w
 
     def end_step(self):
         """After every bucket of the step was waited on: no rank may overwrite its gradient
         buffer (next backward) before every peer finished reading it."""
+        if self.eng is not None:
+            self.eng.end_step(torch.cuda.current_stream(self.dev).cuda_stream)
+            self.seq += 1
+            return
         done = threading.Event()
         self.q.put(("step", done))
         done.wait()
