@@ -168,19 +168,24 @@ class XgmiEngine {
   }
   int64_t seq() const { return seq_; }
 
-  // backward thread: bucket b's gradients are enqueued on `cur`
-  void launch(int b, uintptr_t cur) {
+  // backward thread: bucket b's gradients are enqueued on `cur`. Returns the step's sequence
+  // number, the ticket wait() takes (a bucket may be waited on after end_step moved to the next)
+  int64_t launch(int b, uintptr_t cur) {
     TORCH_CHECK(b >= 0 && b < nb_, "XgmiEngine.launch: bucket index");
     hchk(hipEventRecord((hipEvent_t)ev_ready_[b], (hipStream_t)cur), "record ready");
     push(b);
+    std::lock_guard<std::mutex> g(mu_);
+    return seq_;
   }
-  // `cur` waits (GPU-side) for bucket b's all-reduce; blocks the host only until the worker has
-  // enqueued it
-  void wait(int b, uintptr_t cur) {
+  // `cur` waits (GPU-side) for bucket b's all-reduce of step `seq`; blocks the host only until the
+  // worker has enqueued it
+  void wait(int b, int64_t seq, uintptr_t cur) {
     {
       py::gil_scoped_release nogil;
       std::unique_lock<std::mutex> g(mu_);
-      cv_done_.wait(g, [&] { return processed_[b] >= seq_ || !err_.empty(); });
+      if (!cv_done_.wait_for(g, std::chrono::seconds(600), [&] { return processed_[b] >= seq || !err_.empty(); }) &&
+          err_.empty())
+        err_ = "bucket " + std::to_string(b) + " of step " + std::to_string(seq) + " not processed in 600 s";
     }
     check_err();
     hchk(hipStreamWaitEvent((hipStream_t)cur, done_[b], 0), "wait done");
@@ -190,7 +195,9 @@ class XgmiEngine {
     {
       py::gil_scoped_release nogil;
       std::unique_lock<std::mutex> g(mu_);
-      cv_done_.wait(g, [&] { return step_done_ >= seq_ || !err_.empty(); });
+      if (!cv_done_.wait_for(g, std::chrono::seconds(600), [&] { return step_done_ >= seq_ || !err_.empty(); }) &&
+          err_.empty())
+        err_ = "step barrier " + std::to_string(seq_) + " not reached in 600 s";
     }
     check_err();
     for (int r = 0; r < world_; ++r)

@@ -77,6 +77,10 @@ class GradReducer:
         self.enabled = True
         flat.reducer = self
         self.timer: Optional["CommTimer"] = None
+        # diagnostic (tools/queue_probe.py): issue the RCCL all-reduce even in a 1-rank group, so a
+        # 1-GPU trace shows the collective's stream beside compute
+        self.force_collective = (os.environ.get("PYRECOVER_FORCE_ALLREDUCE") == "1" and dist.is_available()
+                                 and dist.is_initialized())
         self.xgmi = None
         if self.backend == "xgmi":
             from .xgmi import XgmiAllReduce
@@ -113,7 +117,7 @@ class GradReducer:
             self.timer.ready(b)
         if self.xgmi is not None:
             work = self.xgmi.launch(b)
-        elif self.world > 1:
+        elif self.world > 1 or self.force_collective:
             work = dist.all_reduce(self.flat.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
             if self.timer is not None:
                 self.timer.launched(b, work)

@@ -63,17 +63,18 @@ def _hidden_ranks(vis) -> List[int]:
     return sorted({r for r, (own, _) in enumerate(vis) for _, seen in vis if own not in seen})
 
 class _Work:
-    __slots__ = ("owner", "b", "ready")
+    __slots__ = ("owner", "b", "ready", "seq")
 
     def __init__(self, owner, b):
         self.owner = owner
         self.b = b
         self.ready = threading.Event()
+        self.seq = 0  # native engine: the step this bucket belongs to (a ticket for wait)
 
     def wait(self):
         """Current stream waits (GPU-side) for the all-reduced bucket."""
         if self.owner.eng is not None:
-            self.owner.eng.wait(self.b, torch.cuda.current_stream(self.owner.dev).cuda_stream)
+            self.owner.eng.wait(self.b, self.seq, torch.cuda.current_stream(self.owner.dev).cuda_stream)
             return
         self.ready.wait()
         if self.owner.error is not None:
@@ -262,7 +263,7 @@ class XgmiAllReduce:
     def launch(self, b: int) -> _Work:
         w = _Work(self, b)
         if self.eng is not None:
-            self.eng.launch(b, torch.cuda.current_stream(self.dev).cuda_stream)
+            w.seq = self.eng.launch(b, torch.cuda.current_stream(self.dev).cuda_stream)
             return w
         self.C.event_record(self.ev_ready[b], torch.cuda.current_stream(self.dev).cuda_stream)
         self.q.put((b, w))
