@@ -798,7 +798,7 @@ PYBIND11_MODULE(_C, m) {
     pra_attn_set_options(fwd_pipe, (float)fwd_thr, dkdv_impl, dq_pipe, dkdv_split, dkdv_kreg);
   }, "attention kernel selection: fwd_pipe / dkdv_impl / dq_pipe = -1 (by shape), 0 or 1; fwd_thr = rescale "
      "threshold (log2); dkdv_split = -1 (by grid) or query-head splits of the pipelined dK/dV kernel; "
-     "dkdv_kreg = 2: ring-staged dK/dV kernel (default), 1: two-wave dK/dV kernel keeps K in registers, 0: K in LDS");
+     "dkdv_kreg = 2: ring-staged dK/dV kernel, -2 (default): ring unless a side-stream job waits for the dK/dV window, 1: two-wave dK/dV kernel keeps K in registers, 0: K in LDS");
   register_ckpt_engine(m);
   register_xgmi(m);
 }

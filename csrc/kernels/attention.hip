@@ -1328,13 +1328,16 @@ struct AttnOptions {
   // the overlapped optimizer, and its fp32 partial sums would make the gradients depend on whether
   // the optimizer overlaps (tests/test_xgmi_gpu.py compares the two bitwise)
   int dkdv_split = 1;
-  // two-wave dK/dV kernel (NW = 8, D = 128): 2 = ring-staged bwd_dkdv_r_kernel (default: K in
-  // registers, Q/dO by LDS-DMA, one barrier per query tile; B16 S2048 H32 bwd 2.39 -> 2.27 ms,
+  // two-wave dK/dV kernel (NW = 8, D = 128): 2 = ring-staged bwd_dkdv_r_kernel (K in registers,
+  // Q/dO by LDS-DMA, one barrier per query tile; B16 S2048 H32 bwd 2.39 -> 2.27 ms,
   // profiles/r5/attn/harness_dkdv_ring.log), 1 = bwd_dkdv_kernel with K fragments held in registers
   // (KREG), 0 = bwd_dkdv_kernel reading K from LDS, -1 = KREG unless a side-stream job waits for the
   // dK/dV window (below) (r4: KREG 2.387 -> 2.358 ms alone, but 1058.0 vs 1055.5 ms in the 7B step:
-  // profiles/r4/attn_ab_dkdv_kreg_b16.log, step_ab_7b_b16_kreg.log)
-  int dkdv_kreg = 2;
+  // profiles/r4/attn_ab_dkdv_kreg_b16.log, step_ab_7b_b16_kreg.log), -2 (default) = the ring kernel
+  // unless a side-stream job waits for the window, else 0: the ring kernel's 242 VGPRs leave no
+  // room on the SIMDs for the overlapped AdamW waves (the LDS kernel's 215 do), so in the overlapped
+  // 7B B16 step it is not faster (1054.7 vs 1053.3 ms, profiles/r5/step_ab_ring.log)
+  int dkdv_kreg = -2;
 };
 AttnOptions g_attn_opts;
 
@@ -1428,7 +1431,8 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
   // (-lse log2(e), -delta), written by the dQ kernel only when that kernel runs
   const long nrc = (long)B * Hq * S;
   const bool p2 = dkdv_use_p2(B, S, Hq, Hkv, D);
-  const bool ring = g_attn_opts.dkdv_kreg == 2 && !p2 && nw == 8 && D == 128;  // bwd_dkdv_r_kernel
+  const bool ring = (g_attn_opts.dkdv_kreg == 2 || (g_attn_opts.dkdv_kreg == -2 && mid_event == nullptr)) && !p2 &&
+                    nw == 8 && D == 128;  // bwd_dkdv_r_kernel
   float* rc2 = (p2 || ring) ? delta + nrc : nullptr;
   // dQ first: it also computes delta = rowsum(dO * O), which the dK/dV kernel reads
   {

@@ -302,12 +302,28 @@ __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, c
   };
 
   if (skG > 0) {
-    // Stream-K: the nwg * nk (tile, k-step) iterations, tile-major, are cut into skG equal ranges,
-    // one per workgroup (one per CU), so every CU gets the same work however nwg divides by the CU
-    // count. A tile covered by several ranges is summed deterministically: each range writes its
-    // fp32 partial to its own slot (2 g: the range's first tile, 2 g + 1: its last), and the last
-    // arriver adds the partials in range order -- the k order -- whoever arrives last.
-    const long W = (long)nwg * nk;
+    // Persistent data-parallel rounds + a stream-K remainder (skG workgroups, one per CU):
+    //  * all but the last round's worth of whole tiles run as data-parallel rounds, every workgroup
+    //    one tile per round in the classic XCD-aware group-M order (the tiles resident together
+    //    share A/B panels in L2);
+    //  * the remaining skG + nwg % skG tiles' (tile, k-step) iterations are cut into skG equal
+    //    ranges, so every CU ends at the same time however nwg divides by the CU count. A tile
+    //    covered by several ranges is summed deterministically: each range writes its fp32 partial
+    //    to its own slot (2 g: the range's first tile, 2 g + 1: its last), and the last arriver adds
+    //    the partials in range order -- the k order -- whoever arrives last.
+    // (Stream-K over ALL tiles spreads the concurrently active tiles over the whole matrix and lost
+    // 35-40% to L2 misses on the 7B W1|W3 / W2 shapes: profiles/r5/wgrad_bench_7b.log.)
+    const int rem = nwg % skG;
+    const int sk_tiles = rem == 0 ? 0 : min(nwg, skG + rem);
+    const int dp_tiles = nwg - sk_tiles;  // a multiple of skG
+    for (int lin0 = 0; lin0 < dp_tiles; lin0 += skG) {
+      long m0, n0;
+      tile_origin(lin0 + xcd_remap(blockIdx.x, skG), tiles_m, tiles_n, m0, n0);
+      run(m0, n0, 0, nk);
+      store_c(m0, n0);
+    }
+    if (sk_tiles == 0) return;
+    const long W = (long)sk_tiles * nk;
     const int g = xcd_remap(blockIdx.x, skG);  // consecutive ranges (adjacent tiles) share an XCD
     auto start = [&](int gg) -> long { return W * gg / skG; };
     auto owner = [&](long x) -> int {  // the range containing iteration x
@@ -320,10 +336,10 @@ __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, c
     const long e = start(g + 1);
     const int first_tile = (int)(s / nk);
     while (s < e) {
-      const int t = (int)(s / nk), kb = (int)(s % nk);
+      const int t = (int)(s / nk), kb = (int)(s % nk);  // t: index among the stream-K tiles
       const int ke = (int)min((long)nk, (long)kb + (e - s));
       long m0, n0;
-      tile_origin(t, tiles_m, tiles_n, m0, n0);
+      tile_origin(dp_tiles + t, tiles_m, tiles_n, m0, n0);
       run(m0, n0, kb, ke);
       if (kb == 0 && ke == nk) {
         store_c(m0, n0);

@@ -9,3 +9,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace -d $O/qprobe -o q -- python3 tools/qu
 python tools/queue_probe.py --summary $(find $O/qprobe -name 'q_results.db' | head -1) > $O/queue_map.md 2>&1; cat $O/queue_map.md
 timeout -k 10 300 python bench.py --model llama3-8b --batch-per-gpu 1 --steps 20 --warmup 5 > $O/bench_8b_b1.log 2>&1 || exit 1
 tail -1 $O/bench_8b_b1.log
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "streamk or dkdv" > $O/pytest_streamk.log 2>&1 || { tail -20 $O/pytest_streamk.log; exit 1; }
+tail -1 $O/pytest_streamk.log
+timeout -k 10 300 python tools/wgrad_bench.py --rounds 3 > $O/wgrad_bench_7b_hybrid.log 2>&1 || exit 1
+grep shape $O/wgrad_bench_7b_hybrid.log
