@@ -1338,6 +1338,9 @@ struct AttnOptions {
   // room on the SIMDs for the overlapped AdamW waves (the LDS kernel's 215 do), so in the overlapped
   // 7B B16 step it is not faster (1054.7 vs 1053.3 ms, profiles/r5/step_ab_ring.log)
   int dkdv_kreg = -2;
+  // fused backward (attention_bwd_fused.hip: dQ, dK, dV in one workgroup per (batch, kv head)):
+  // -1 = by shape (attn_bwd_use_fused), 0 = never (split dQ + dK/dV kernels), 1 = whenever it applies
+  int bwd_fused = -1;
 };
 AttnOptions g_attn_opts;
 
@@ -1405,13 +1408,38 @@ static int dkdv_split(int B, int S, int Hq, int Hkv, int D) {
   return (n >= 1 && nrep % n == 0) ? n : 1;
 }
 
+// Fused backward (attention_bwd_fused.hip) applies at D = 128, S % 256 == 0 without key padding. By
+// shape it runs when its grid -- one workgroup per (batch, kv head), each walking all S / 256 key
+// blocks -- fills whole rounds of the chip (>= 90% of the slots of its last round busy): 7B-class MHA
+// at batch >= 8. Its choice never depends on the AdamW window (mid_event), so overlapped and plain
+// optimizer steps see the same gradients.
+static int device_cus() {
+  static int cus[64] = {0};
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) return 256;
+  if (cus[d] == 0 && (hipDeviceGetAttribute(&cus[d], hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || cus[d] <= 0))
+    cus[d] = 256;
+  return cus[d];
+}
+static bool fused_shape_ok(int S, int D) { return D == 128 && S % 256 == 0; }
+static bool attn_bwd_use_fused(int B, int S, int Hq, int Hkv, int D, int skv) {
+  const int mode = g_attn_opts.bwd_fused;
+  if (mode == 0 || !fused_shape_ok(S, D) || skv != S) return false;
+  if (mode == 1) return true;
+  const long grid = (long)B * Hkv, cus = device_cus();
+  const long rounds = (grid + cus - 1) / cus;
+  return grid >= cus && grid * 10 >= rounds * cus * 9;
+}
+
 // fp32 workspace of pra_attn_bwd, in floats: delta, the row constants (-lse log2(e), -delta) of the
-// pipelined dK/dV kernel, and its split partials
+// pipelined dK/dV kernel and the fused kernel, the dK/dV split partials, or the fused kernel's dQ partials
 long attn_bwd_ws_floats(int B, int S, int Hq, int Hkv, int D) {
   const long nrc = (long)B * Hq * S;
   const bool p2 = dkdv_use_p2(B, S, Hq, Hkv, D);
   const int n = p2 ? dkdv_split(B, S, Hq, Hkv, D) : 1;
-  return 3 * nrc + (n > 1 ? 2L * n * B * S * Hkv * D : 0);
+  const long split = 3 * nrc + (n > 1 ? 2L * n * B * S * Hkv * D : 0);
+  const long fused = g_attn_opts.bwd_fused != 0 && fused_shape_ok(S, D) ? 3 * nrc + nrc * D + 1024L * B * Hkv : 0;
+  return split > fused ? split : fused;
 }
 
 template <typename T>
@@ -1424,6 +1452,13 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
   const float2* rt = reinterpret_cast<const float2*>(rope_tab);
   if (ldq % 8 || ldk % 8 || ldv % 8 || ldo % 8 || lddo % 8 || lddq % 8 || lddk % 8 || lddv % 8)
     return hipErrorInvalidValue;
+  if (attn_bwd_use_fused(B, S, Hq, Hkv, D, skv)) {
+    if (mid_event != nullptr) hipEventRecord(mid_event, st);  // the window spans the whole fused kernel
+    const long nrc = (long)B * Hq * S;
+    return pra_attn_bwd_fused(std::is_same<T, __bf16>::value ? pra::kBF16 : pra::kF16, q, k, v, o, dout, lse,
+                              delta + nrc, dq, dk, dv, B, S, Hq, Hkv, ldq, ldk, ldv, ldo, lddo, lddq, lddk, lddv,
+                              scale, causal, rope_tab, st);
+  }
   const float sl2 = scale * 1.4426950408889634f;
   // 8-wave (256-row) blocks; S % 256 != 0 (S % 128 == 0) takes the 4-wave instantiations
   const int nw = S % 256 ? 4 : 8;
@@ -1549,7 +1584,9 @@ hipError_t pra_attn_bwd(int dtype, const void* q, const void* k, const void* v, 
 }
 
 // Kernel selection (see AttnOptions); not thread-safe against concurrent launches (set between steps).
-void pra_attn_set_options(int fwd_pipe, float fwd_thr, int dkdv_impl, int dq_pipe, int dkdv_split, int dkdv_kreg) {
+void pra_attn_set_options(int fwd_pipe, float fwd_thr, int dkdv_impl, int dq_pipe, int dkdv_split, int dkdv_kreg,
+                          int bwd_fused) {
+  g_attn_opts.bwd_fused = bwd_fused;
   g_attn_opts.fwd_pipe = fwd_pipe;
   g_attn_opts.fwd_thr = fwd_thr;
   g_attn_opts.dkdv_impl = dkdv_impl;

@@ -183,6 +183,18 @@ struct Stage {
         r[i] = make_uint4(0, 0, 0, 0);
     }
   }
+  // every row in bounds (no per-row branch: the load count is a compile-time constant, so counted
+  // vmcnt waits stay exact across it)
+  __device__ __forceinline__ void load_all(const T* g, long ld, int row0) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int idx = i * NT + threadIdx.x;
+      if (!EXACT && idx >= ROWS * CH) continue;
+      int row, c;
+      rc(idx, row, c);
+      r[i] = *reinterpret_cast<const uint4*>(g + (long)(row0 + row) * ld + c * 8);
+    }
+  }
   __device__ __forceinline__ void store(T* tile) const {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {

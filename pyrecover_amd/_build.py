@@ -58,7 +58,8 @@ def _run(cmd):
 # MFMAs costs more issue cycles than the scalar form).
 # -amdgpu-mfma-vgpr-form: the one-wave-per-SIMD backward kernel keeps its loop-carried dK/dV sums in
 # VGPRs; with AGPR-form MFMAs the compiler copies them between the two files around every step.
-EXTRA_FLAGS = {"attention.hip": ["-fno-honor-nans", "-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"]}
+EXTRA_FLAGS = {"attention.hip": ["-fno-honor-nans", "-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"],
+               "attention_bwd_fused.hip": ["-fno-honor-nans", "-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"]}
 
 
 def build(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:

@@ -32,4 +32,5 @@ def attn_opts(cuda):
     from pyrecover_amd import _ext
 
     yield _ext.set_attn_options
-    _ext.set_attn_options(fwd_pipe=None, fwd_thr=None, dkdv_impl=None, dq_pipe=None, dkdv_split=None, dkdv_kreg=None)
+    _ext.set_attn_options(fwd_pipe=None, fwd_thr=None, dkdv_impl=None, dq_pipe=None, dkdv_split=None, dkdv_kreg=None,
+                          bwd_fused=None)

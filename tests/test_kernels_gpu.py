@@ -377,6 +377,46 @@ def test_attention_bwd_fused_inverse_rope(cuda, attn_opts, impl, B, S, Hq, Hkv, 
         assert _rel(got, sep.view(B, S, H, D).float()) < 1e-2
 
 
+@pytest.mark.parametrize("B,S,Hq,Hkv,causal,rope", [(1, 1024, 4, 1, True, True), (2, 512, 4, 2, False, True),
+                                                    (2, 768, 3, 3, True, False), (1, 256, 2, 2, False, False)])
+def test_attention_bwd_fused_kernel(cuda, attn_opts, B, S, Hq, Hkv, causal, rope):
+    """attention_bwd_fused.hip (dQ, dK, dV of a (batch, kv head) in one workgroup; dQ summed over the
+    key blocks in order through an fp32 workspace): against the fp32 oracle (with the inverse RoPE on
+    dq / dk), multi-block causal and full attention, GQA; bitwise deterministic run to run; dV bitwise
+    equal to the split ring-staged dK/dV kernel (same P)."""
+    from pyrecover_amd.ops.reference import precompute_freqs_cis, rope_table
+
+    D = 128
+    C = _ext.native()
+    _, q, k, v = _qkv(cuda, B, S, Hq, Hkv, D, seed=13)
+    scale = 1 / math.sqrt(D)
+    tab = rope_table(precompute_freqs_cis(D, S, 10000.0)).to(cuda) if rope else None
+    o, lse = C.attn_fwd(q, k, v, scale, causal)
+    do = torch.randn(B, S, Hq, D, device=cuda).bfloat16()
+    outs = []
+    for fused in (1, 1, 0):
+        attn_opts(bwd_fused=fused, dkdv_kreg=2, dkdv_impl=0)
+        d3 = [torch.full_like(t, float("nan")) for t in (q, k, v)]
+        C.attn_bwd(q, k, v, o, do, lse, *d3, scale, causal, tab)
+        outs.append(d3)
+    (dq, dk, dv), again, split = outs
+    assert all(torch.equal(a, b) for a, b in zip((dq, dk, dv), again))
+    assert torch.equal(dv, split[2])
+    qf, kf, vf = (t.float().requires_grad_() for t in (q, k, v))
+    of, _ = R.attention_lse_ref(qf, kf, vf, causal, scale)
+    of.backward(do.float())
+    for got, g32, H in ((dq, qf.grad, Hq), (dk, kf.grad, Hkv), (dv, vf.grad, Hkv)):
+        want = g32
+        if rope and got is not dv:
+            want = g32.reshape(B * S, H * D).clone()
+            R.rope_inplace_2d(want, H * D, tab, D, S, inverse=True)
+            want = want.view(B, S, H, D)
+        assert torch.isfinite(got.float()).all()
+        assert _rel(got, want) < 3e-2, _rel(got, want)
+    for got, base in zip((dq, dk), split[:2]):
+        assert _rel(got, base.float()) < 1e-2
+
+
 @pytest.mark.parametrize("T,F,dtype", [(4096, 1024, torch.bfloat16), (1000, 392, torch.bfloat16),
                                        (512, 256, torch.float16), (256, 136, torch.float32)])
 def test_swiglu_bwd_variants_bitwise(cuda, T, F, dtype):

@@ -18,7 +18,9 @@ for spec in "$@"; do
   defs=${spec#*=}
   ( $HIPCC $FL $AFL -DPRA_ATTN_HARNESS=1 $defs -c csrc/kernels/attention.hip -o $OUT/attention_$name.o \
       -Rpass-analysis=kernel-resource-usage 2> $OUT/attention_$name.res \
-    && $HIPCC $FL $OUT/harness.o $OUT/attention_$name.o $OUT/attention_f32.o -o $OUT/attn_$name \
+    && $HIPCC $FL $AFL -DPRA_ATTN_HARNESS=1 $defs -c csrc/kernels/attention_bwd_fused.hip -o $OUT/fused_$name.o \
+      -Rpass-analysis=kernel-resource-usage 2> $OUT/fused_$name.res \
+    && $HIPCC $FL $OUT/harness.o $OUT/attention_$name.o $OUT/fused_$name.o $OUT/attention_f32.o -o $OUT/attn_$name \
     && echo "built $OUT/attn_$name" ) &
   pids+=($!)
 done
