@@ -1339,8 +1339,12 @@ struct AttnOptions {
   // 7B B16 step it is not faster (1054.7 vs 1053.3 ms, profiles/r5/step_ab_ring.log)
   int dkdv_kreg = -2;
   // fused backward (attention_bwd_fused.hip: dQ, dK, dV in one workgroup per (batch, kv head)):
-  // -1 = by shape (attn_bwd_use_fused), 0 = never (split dQ + dK/dV kernels), 1 = whenever it applies
-  int bwd_fused = -1;
+  // -1 = by shape (attn_bwd_use_fused), 0 = never (split dQ + dK/dV kernels; the default), 1 = whenever
+  // it applies. Not the default: alone it is faster (7B B16 step without the AdamW update 1032.7 ->
+  // 1025.7 ms), but its 256-VGPR waves leave no room for the overlapped update's waves, which the split
+  // dK/dV kernel hosts (with the update 1045.4 vs 1048.3 ms; profiles/r5/attn_fused/). The choice must
+  // not depend on the window (dQ differs in the last bits), so it is a run-wide setting.
+  int bwd_fused = 0;
 };
 AttnOptions g_attn_opts;
 
@@ -1453,11 +1457,11 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
   if (ldq % 8 || ldk % 8 || ldv % 8 || ldo % 8 || lddo % 8 || lddq % 8 || lddk % 8 || lddv % 8)
     return hipErrorInvalidValue;
   if (attn_bwd_use_fused(B, S, Hq, Hkv, D, skv)) {
-    if (mid_event != nullptr) hipEventRecord(mid_event, st);  // the window spans the whole fused kernel
+    // the window (mid_event) opens after the memory-bound row-constant pass, beside the fused kernel
     const long nrc = (long)B * Hq * S;
     return pra_attn_bwd_fused(std::is_same<T, __bf16>::value ? pra::kBF16 : pra::kF16, q, k, v, o, dout, lse,
                               delta + nrc, dq, dk, dv, B, S, Hq, Hkv, ldq, ldk, ldv, ldo, lddo, lddq, lddk, lddv,
-                              scale, causal, rope_tab, st);
+                              scale, causal, rope_tab, mid_event, st);
   }
   const float sl2 = scale * 1.4426950408889634f;
   // 8-wave (256-row) blocks; S % 256 != 0 (S % 128 == 0) takes the 4-wave instantiations

@@ -35,21 +35,21 @@ namespace pra {
 namespace attn {
 
 // RC[i] = -lse[i] log2(e), RC[nrc + i] = -delta[i], delta = rowsum(dO * O); i = (b Hq + hq) S + q.
-// 16 lanes per row (8 elements each at D = 128).
+// 16 lanes per row (8 elements each at D = 128), rows in TOKEN order (t Hq + hq), so a wave reads
+// 4 consecutive 256-B head rows of one token: in (b, hq, q) order consecutive rows were a token
+// stride (8 KiB at 7B) apart and the pass took 0.47 ms instead of ~0.1 at B16 S2048 H32.
 template <typename T>
 __global__ __launch_bounds__(256) void bwd_rowc_kernel(const T* __restrict__ O, const T* __restrict__ dO,
                                                        const float* __restrict__ LSE, float* __restrict__ RC,
                                                        long nrc, int S, int Hq, long ldo, long lddo) {
   constexpr int D = 128;
-  const long row = ((long)blockIdx.x * 256 + threadIdx.x) >> 4;
+  const long row = ((long)blockIdx.x * 256 + threadIdx.x) >> 4;  // token-major: tok Hq + hq
   const int sub = threadIdx.x & 15;
   const long r = row < nrc ? row : nrc - 1;  // (nrc % 16 == 0: whole groups; clamp keeps the shuffles uniform)
-  const int q = (int)(r % S);
-  const long bh = r / S;
-  const int hq = (int)(bh % Hq);
-  const long b = bh / Hq;
-  const V8<T> o8 = *reinterpret_cast<const V8<T>*>(O + (b * S + q) * ldo + hq * D + 8 * sub);
-  const V8<T> d8 = *reinterpret_cast<const V8<T>*>(dO + (b * S + q) * lddo + hq * D + 8 * sub);
+  const long tok = r / Hq;
+  const int hq = (int)(r % Hq);
+  const V8<T> o8 = *reinterpret_cast<const V8<T>*>(O + tok * ldo + hq * D + 8 * sub);
+  const V8<T> d8 = *reinterpret_cast<const V8<T>*>(dO + tok * lddo + hq * D + 8 * sub);
   float part = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) part = fmaf((float)o8[j], (float)d8[j], part);
@@ -58,8 +58,10 @@ __global__ __launch_bounds__(256) void bwd_rowc_kernel(const T* __restrict__ O, 
   part += __shfl_xor(part, 2, 16);
   part += __shfl_xor(part, 1, 16);
   if (sub == 0 && row < nrc) {
-    RC[row] = -LSE[row] * 1.4426950408889634f;
-    RC[nrc + row] = -part;
+    const long b = tok / S, q = tok % S;
+    const long i = (b * Hq + hq) * S + q;
+    RC[i] = -LSE[i] * 1.4426950408889634f;
+    RC[nrc + i] = -part;
   }
 }
 
@@ -277,7 +279,8 @@ extern "C" {
 hipError_t pra_attn_bwd_fused(int dtype, const void* q, const void* k, const void* v, const void* o, const void* dout,
                               const float* lse, float* ws, void* dq, void* dk, void* dv, int B, int S, int Hq,
                               int Hkv, long ldq, long ldk, long ldv, long ldo, long lddo, long lddq, long lddk,
-                              long lddv, float scale, int causal, const float* rope_tab, hipStream_t st) {
+                              long lddv, float scale, int causal, const float* rope_tab, hipEvent_t mid_event,
+                              hipStream_t st) {
   using namespace pra::attn;
   if (S % 256 || S <= 0 || Hq % Hkv || B <= 0) return hipErrorInvalidValue;
   if (ldq % 8 || ldk % 8 || ldv % 8 || ldo % 8 || lddo % 8 || lddq % 8 || lddk % 8 || lddv % 8)
@@ -291,6 +294,7 @@ hipError_t pra_attn_bwd_fused(int dtype, const void* q, const void* k, const voi
 #define PRA_FUSED(TT)                                                                                          \
   hipLaunchKernelGGL((bwd_rowc_kernel<TT>), g0, dim3(256), 0, st, (const TT*)o, (const TT*)dout, lse, rc, nrc, S, \
                      Hq, ldo, lddo);                                                                           \
+  if (mid_event != nullptr) hipEventRecord(mid_event, st);                                                     \
   if (causal)                                                                                                  \
     hipLaunchKernelGGL((bwd_fused_kernel<TT, true>), g1, dim3(512), 0, st, (const TT*)q, (const TT*)k,         \
                        (const TT*)v, (const TT*)dout, rc, nrc, (TT*)dq, (TT*)dk, (TT*)dv, acc, S, Hq, Hkv, ldq,  \

@@ -94,7 +94,8 @@ void pra_attn_set_options(int fwd_pipe, float fwd_thr, int dkdv_impl, int dq_pip
 hipError_t pra_attn_bwd_fused(int dtype, const void* q, const void* k, const void* v, const void* o, const void* dout,
                               const float* lse, float* ws, void* dq, void* dk, void* dv, int B, int S, int Hq,
                               int Hkv, long ldq, long ldk, long ldv, long ldo, long lddo, long lddq, long lddk,
-                              long lddv, float scale, int causal, const float* rope_tab, hipStream_t st);
+                              long lddv, float scale, int causal, const float* rope_tab, hipEvent_t mid_event,
+                              hipStream_t st);
 // floats of fp32 workspace pra_attn_bwd needs at `delta` (delta, row constants, split dK/dV parts)
 long pra_attn_bwd_workspace(int dtype, int B, int S, int Hq, int Hkv, int D);
 // fp32 flash attention (attention_f32.hip, f32-input MFMA); pra_attn_fwd / pra_attn_bwd route kF32 here

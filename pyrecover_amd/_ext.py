@@ -68,7 +68,7 @@ def hip16(t) -> bool:
 # read no environment; PYRECOVER_ATTN_{FWD_PIPE,FWD_THR,DKDV_IMPL,DQ_PIPE,DKDV_SPLIT,DKDV_KREG} are read once here, when
 # the extension loads, and set_attn_options() changes them between launches (tests, A/B tools).
 _ATTN_DEFAULTS = {"fwd_pipe": -1, "fwd_thr": 8.0, "dkdv_impl": -1, "dq_pipe": -1, "dkdv_split": 1, "dkdv_kreg": -2,
-                  "bwd_fused": -1}
+                  "bwd_fused": 0}
 _attn_opts = dict(_ATTN_DEFAULTS)
 
 

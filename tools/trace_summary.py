@@ -35,6 +35,8 @@ def main():
         key = name[:90]
         if gemm:
             key = "GEMM " + (f"grid {r['Grid_Size_X']}x{r['Grid_Size_Y']}x{r['Grid_Size_Z']} " if a.by_grid else "") + name.split("_MT")[1][:20] if "_MT" in name else name[:60]
+        elif a.by_grid and ("wgrad" in name or "gemm_nt" in name or "attn" in name):
+            key = f"{name[:60]} grid {r['Grid_Size_X']}"
         per[key][0] += d / a.steps
         per[key][1] += 1
         per_stream[r["Queue_Id"]] += d / a.steps
