@@ -65,8 +65,25 @@ __global__ __launch_bounds__(256) void bwd_rowc_kernel(const T* __restrict__ O, 
   }
 }
 
+// Variant switches (tools/attn_variants.sh). PRA_FUSED_MAXV=112 caps the kernel at 224 VGPRs
+// (amdgpu_num_vgpr counts VGPR + AGPR pairs on gfx90a+), so one 64-VGPR wave of the overlapped AdamW
+// update fits on each SIMD beside it; with PRA_FUSED_LATE_ACC=1 the dQ partial is read after the dS
+// barrier instead of held in 16 registers across the tile. Measured (profiles/r5/attn_fused/): alone
+// 2.28 vs 2.21 ms, and the overlapped 7B step did not improve (1063.3 vs 1058.7 ms split), so both off.
+#ifndef PRA_FUSED_LATE_ACC
+#define PRA_FUSED_LATE_ACC 0
+#endif
+#ifndef PRA_FUSED_MAXV
+#define PRA_FUSED_MAXV 0
+#endif
+#if PRA_FUSED_MAXV
+#define PRA_FUSED_VGPR_ATTR __attribute__((amdgpu_num_vgpr(PRA_FUSED_MAXV)))
+#else
+#define PRA_FUSED_VGPR_ATTR
+#endif
+
 template <typename T, bool CAUSAL>
-__global__ __launch_bounds__(512, 1) void bwd_fused_kernel(
+__global__ __launch_bounds__(512, 1) PRA_FUSED_VGPR_ATTR void bwd_fused_kernel(
     const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V, const T* __restrict__ dO,
     const float* __restrict__ RC, long nrc, T* __restrict__ dQ, T* __restrict__ dK, T* __restrict__ dV,
     float* __restrict__ dQacc, int S, int Hq, int Hkv, long ldq, long ldk, long ldv, long lddo, long lddq,
@@ -165,7 +182,8 @@ __global__ __launch_bounds__(512, 1) void bwd_fused_kernel(
       float* const slot = dQacc + ((((long)b * Hq + hq) * nqs + q0 / QT) * 4 + (wid & 3)) * 1024 + 4 * lane;
       const bool real = wid < 4 && !first;
       const float* src = real ? slot : scratch;
-      f32x16 acc;
+      f32x16 acc = f32x16{};
+#if !PRA_FUSED_LATE_ACC
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float4 v = *reinterpret_cast<const float4*>(src + 256 * i);
@@ -174,6 +192,7 @@ __global__ __launch_bounds__(512, 1) void bwd_fused_kernel(
         acc[4 * i + 2] = real ? v.z : 0.f;
         acc[4 * i + 3] = real ? v.w : 0.f;
       }
+#endif
       sq.store(Qs);
       sd.store(Ds);
       __syncthreads();  // Q / dO of this tile (and, at it = 0, the block's scaled K) visible
@@ -232,6 +251,13 @@ __global__ __launch_bounds__(512, 1) void bwd_fused_kernel(
         for (int g = 0; g < 4; ++g) sput(g, make_uint2(0u, 0u));
       }
       __syncthreads();  // dS of all 256 keys in LDS
+#if PRA_FUSED_LATE_ACC
+      // the partial is read here (under the 16 MFMAs below) instead of held in 16 registers across
+      // the tile: fewer VGPRs, so a wave of the overlapped AdamW update fits beside the block
+      float4 pv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pv[i] = *reinterpret_cast<const float4*>(src + 256 * i);
+#endif
       if (wid < 4) {
         V8<T> ka = lo.tr(Ks, 0, wid), sb = ls.tr(Ss, 0, 0);
 #pragma unroll
@@ -246,6 +272,15 @@ __global__ __launch_bounds__(512, 1) void bwd_fused_kernel(
           sb = ns;
         }
       }
+#if PRA_FUSED_LATE_ACC
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        acc[4 * i] += real ? pv[i].x : 0.f;
+        acc[4 * i + 1] += real ? pv[i].y : 0.f;
+        acc[4 * i + 2] += real ? pv[i].z : 0.f;
+        acc[4 * i + 3] += real ? pv[i].w : 0.f;
+      }
+#endif
       if (wid < 4 && last) {
         const f32x16 fin[1] = {acc};
         store_rows16<T, 1>(fin, ln2, dQ + ((long)b * S + q0 + l32) * lddq + hq * D + 32 * wid, true, h2,
