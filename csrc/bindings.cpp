@@ -795,12 +795,12 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("scale"), pybind11::arg("causal"), pybind11::arg("rope_tab") = pybind11::none(),
         pybind11::arg("mid_event") = 0);
   m.def("attn_set_options", [](int fwd_pipe, double fwd_thr, int dkdv_impl, int dq_pipe, int dkdv_split, int dkdv_kreg,
-                               int bwd_fused) {
-    pra_attn_set_options(fwd_pipe, (float)fwd_thr, dkdv_impl, dq_pipe, dkdv_split, dkdv_kreg, bwd_fused);
+                               int bwd_fused, int bwd_window) {
+    pra_attn_set_options(fwd_pipe, (float)fwd_thr, dkdv_impl, dq_pipe, dkdv_split, dkdv_kreg, bwd_fused, bwd_window);
   }, "attention kernel selection: fwd_pipe / dkdv_impl / dq_pipe = -1 (by shape), 0 or 1; fwd_thr = rescale "
      "threshold (log2); dkdv_split = -1 (by grid) or query-head splits of the pipelined dK/dV kernel; "
      "dkdv_kreg = 2: ring-staged dK/dV kernel, -2 (default): ring unless a side-stream job waits for the dK/dV window, 1: two-wave dK/dV kernel keeps K in registers, 0: K in LDS; "
-     "bwd_fused = -1 (by shape), 0 (split kernels) or 1: fused dQ/dK/dV kernel");
+     "bwd_fused = -1 (by shape), 0 (split kernels) or 1: fused dQ/dK/dV kernel; bwd_window = 0: side-stream window between dQ and dK/dV, 1: before dQ");
   register_ckpt_engine(m);
   register_xgmi(m);
 }

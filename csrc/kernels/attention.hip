@@ -1345,6 +1345,9 @@ struct AttnOptions {
   // dK/dV kernel hosts (with the update 1045.4 vs 1048.3 ms; profiles/r5/attn_fused/). The choice must
   // not depend on the window (dQ differs in the last bits), so it is a run-wide setting.
   int bwd_fused = 0;
+  // where the side-stream window (mid_event) opens in the split backward: 0 = between the dQ and the
+  // dK/dV kernels (default), 1 = before the dQ kernel (the update then runs beside both)
+  int bwd_window = 0;
 };
 AttnOptions g_attn_opts;
 
@@ -1474,6 +1477,7 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
                     nw == 8 && D == 128;  // bwd_dkdv_r_kernel
   float* rc2 = (p2 || ring) ? delta + nrc : nullptr;
   // dQ first: it also computes delta = rowsum(dO * O), which the dK/dV kernel reads
+  if (mid_event != nullptr && g_attn_opts.bwd_window == 1) hipEventRecord(mid_event, st);
   {
     dim3 grid((S / (32 * nw)) * Hq * B);
     // the pipelined kernel has no key bound: padded non-causal sequences take the plain one
@@ -1496,7 +1500,7 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
     }
 #undef LAUNCH
   }
-  if (mid_event != nullptr) hipEventRecord(mid_event, st);  // between the dQ and dK/dV launches
+  if (mid_event != nullptr && g_attn_opts.bwd_window != 1) hipEventRecord(mid_event, st);  // between dQ and dK/dV
   const bool window = mid_event != nullptr;
   if (p2) {
     const int ns = window && g_attn_opts.dkdv_split < 0 ? 1 : dkdv_split(B, S, Hq, Hkv, D);
@@ -1589,8 +1593,9 @@ hipError_t pra_attn_bwd(int dtype, const void* q, const void* k, const void* v, 
 
 // Kernel selection (see AttnOptions); not thread-safe against concurrent launches (set between steps).
 void pra_attn_set_options(int fwd_pipe, float fwd_thr, int dkdv_impl, int dq_pipe, int dkdv_split, int dkdv_kreg,
-                          int bwd_fused) {
+                          int bwd_fused, int bwd_window) {
   g_attn_opts.bwd_fused = bwd_fused;
+  g_attn_opts.bwd_window = bwd_window;
   g_attn_opts.fwd_pipe = fwd_pipe;
   g_attn_opts.fwd_thr = fwd_thr;
   g_attn_opts.dkdv_impl = dkdv_impl;

@@ -329,7 +329,7 @@ hipError_t pra_attn_bwd_fused(int dtype, const void* q, const void* k, const voi
 #define PRA_FUSED(TT)                                                                                          \
   hipLaunchKernelGGL((bwd_rowc_kernel<TT>), g0, dim3(256), 0, st, (const TT*)o, (const TT*)dout, lse, rc, nrc, S, \
                      Hq, ldo, lddo);                                                                           \
-  if (mid_event != nullptr) hipEventRecord(mid_event, st);                                                     \
+  if (mid_event != nullptr && hipEventRecord(mid_event, st) != hipSuccess) return hipErrorInvalidResourceHandle; \
   if (causal)                                                                                                  \
     hipLaunchKernelGGL((bwd_fused_kernel<TT, true>), g1, dim3(512), 0, st, (const TT*)q, (const TT*)k,         \
                        (const TT*)v, (const TT*)dout, rc, nrc, (TT*)dq, (TT*)dk, (TT*)dv, acc, S, Hq, Hkv, ldq,  \
