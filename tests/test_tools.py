@@ -1,0 +1,67 @@
+"""CPU tests of the measurement tools whose output the README quotes: the exposed-communication
+model of tools/comm_predict.py and the per-step kernel breakdown of tools/trace_summary.py."""
+import csv
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+
+def test_comm_predict_simulate_in_order_stream():
+    from comm_predict import simulate
+
+    gb = 1e9
+    # two 1 GB buckets, 8 ranks, 100 GB/s bus bandwidth, no latency: each all-reduce takes
+    # 2 * 7/8 * 1 GB / 100 GB/s = 17.5 ms; the second waits for the first (in-order stream)
+    exposed, ends = simulate(ready=[10.0, 12.0], bwd_end=20.0, nbytes=[gb, gb], world=8, busbw_gbps=100.0,
+                             latency_us=0.0)
+    assert ends == pytest.approx([27.5, 45.0])
+    assert exposed == pytest.approx(25.0)
+    # a bucket that is ready after the previous one finished starts at its ready time
+    exposed, ends = simulate([0.0, 50.0], 60.0, [gb, gb], 8, 100.0, 0.0)
+    assert ends == pytest.approx([17.5, 67.5])
+    assert exposed == pytest.approx(7.5)
+    # fully hidden: nothing exposed; per-collective latency is added to every bucket
+    exposed, ends = simulate([0.0], 100.0, [gb], 8, 100.0, 1000.0)
+    assert ends == pytest.approx([18.5]) and exposed == 0.0
+
+
+def _write_trace(path, rows):
+    cols = ["Kernel_Name", "Start_Timestamp", "End_Timestamp", "Queue_Id", "Grid_Size_X", "Grid_Size_Y",
+            "Grid_Size_Z"]
+    with open(path, "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=cols)
+        w.writeheader()
+        for r in rows:
+            w.writerow(dict(zip(cols, r)))
+
+
+def test_trace_summary_steps_and_grid_split(tmp_path):
+    ms = 1_000_000  # ns
+    rows = []
+    t = 0
+    for step in range(3):
+        rows.append(("pra::embed_fwd_kernel<bf16>", t, t + 1 * ms, 1, 256, 1, 1))
+        rows.append(("Cijk_Ailk_Bljk_BBS_BH_MT256x256x64_MI16x16x1_foo", t + 1 * ms, t + 5 * ms, 1, 65536, 1, 1))
+        rows.append(("Cijk_Ailk_Bljk_BBS_BH_MT256x256x64_MI16x16x1_foo", t + 5 * ms, t + 7 * ms, 1, 1024, 1, 1))
+        rows.append(("pra::wg::wgrad16_kernel<bf16>", t + 7 * ms, t + 9 * ms, 1, 2048, 1, 1))
+        rows.append(("pra::adamw_t_kernel<bf16>", t + 7 * ms, t + 8 * ms, 2, 4096, 1, 1))
+        t += 10 * ms
+    rows.append(("pra::embed_fwd_kernel<bf16>", t, t + ms, 1, 256, 1, 1))
+    trace = tmp_path / "t_kernel_trace.csv"
+    _write_trace(trace, rows)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "trace_summary.py"), str(trace), "--steps", "2"],
+                         capture_output=True, text=True, check=True).stdout
+    head = out.splitlines()[0]
+    assert "step wall 10.0 ms" in head and "GEMM 6.0 ms" in head
+    assert "'2': 1.0" in head  # the side queue's AdamW time per step
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "trace_summary.py"), str(trace), "--steps", "2",
+                          "--by-grid"], capture_output=True, text=True, check=True).stdout
+    lines = out.splitlines()
+    assert any(line.startswith("4.00,1,GEMM grid 65536x1x1") for line in lines)
+    assert any(line.startswith("2.00,1,GEMM grid 1024x1x1") for line in lines)
+    assert any("wgrad16_kernel" in line and "grid 2048" in line for line in lines)
