@@ -27,6 +27,13 @@ import time
 import torch
 
 
+def _bucket_arg(v):
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from pyrecover_amd.parallel.bucket_tune import parse_bucket_arg
+
+    return parse_bucket_arg(v)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -35,7 +42,8 @@ def parse():
     ap.add_argument("--model", default="llama2-7b")
     ap.add_argument("--seq-len", type=int, default=2048)
     ap.add_argument("--batch-per-gpu", type=int, default=16)
-    ap.add_argument("--bucket-mb", type=float, default=256.0)
+    ap.add_argument("--bucket-mb", type=_bucket_arg, default=256.0,
+                    help="all-reduce bucket MiB, or 'auto' (startup probe: parallel/bucket_tune.py)")
     ap.add_argument("--lr", type=float, default=1e-5)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--profile-steps", type=int, default=0, help="emit roctx ranges for this many steps")
@@ -151,6 +159,11 @@ def main():
     flat = model.flatten_(tokens_per_step=args.batch_per_gpu * args.seq_len)
     if world > 1:
         broadcast_flat(flat)
+    bucket_tune = None
+    if args.bucket_mb == "auto":
+        from pyrecover_amd.parallel.bucket_tune import autotune_bucket_mb
+
+        args.bucket_mb, bucket_tune = autotune_bucket_mb(dev, flat.grad.dtype)
     reducer = GradReducer(flat, bucket_cap_mb=args.bucket_mb, backend=args.allreduce)
     timer = reducer.enable_comm_timing() if world > 1 and not args.no_comm_timing else None
     opt = FlatAdamW(flat, lr=args.lr, fused=True, grad_scale=1.0 / world)
@@ -260,6 +273,7 @@ def main():
             "config": {"model": f"{args.model}-shape ({n_params / 1e9:.2f}B params)", "global_batch": B * world,
                        "seq_len": S, "parallelism": f"dp{world}", "batch_per_gpu": B,
                        "bucket_mb": args.bucket_mb if world > 1 else None,
+                       "bucket_autotune": bucket_tune,
                        "allreduce": (None if world == 1 else "xgmi" if args.allreduce == "xgmi" else
                                      "rccl" if torch.distributed.get_backend() == "nccl" else
                                      torch.distributed.get_backend()),

@@ -16,6 +16,12 @@ PRECISION_STR_TO_DTYPE = {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32":
                           "fp64": torch.float64}
 
 
+
+def _bucket_arg(v):
+    from .parallel.bucket_tune import parse_bucket_arg
+
+    return parse_bucket_arg(v)
+
 def init_logger():
     """reference utils.py:19-27 (root logger at INFO with the same format)."""
     root = logging.getLogger()
@@ -86,7 +92,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--synthetic-data", action="store_true", help="deterministic random tokens instead of parquet")
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--num-workers", type=int, default=2, help="DataLoader workers (tokenization off the hot loop)")
-    p.add_argument("--bucket-cap-mb", type=float, default=256.0, help="DDP all-reduce bucket size")
+    p.add_argument("--bucket-cap-mb", type=_bucket_arg, default=256.0,
+                   help="DDP all-reduce bucket size in MiB, or 'auto': probe the job's all-reduce latency and "
+                        "bandwidth at startup and pick the size (parallel/bucket_tune.py)")
     p.add_argument("--allreduce", choices=["rccl", "xgmi"], default="rccl",
                    help="gradient all-reduce backend: RCCL rings (default) or the direct per-link xGMI "
                         "reduce-scatter/all-gather over IPC-mapped peer buffers (single node)")

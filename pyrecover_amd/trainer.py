@@ -224,8 +224,14 @@ def train(args):
     reducer = None
     if is_dist:
         broadcast_flat(flat)
+    bucket_mb = args.bucket_cap_mb
+    if bucket_mb == "auto":
+        from .parallel.bucket_tune import autotune_bucket_mb
+
+        bucket_mb, tune = autotune_bucket_mb(device, flat.grad.dtype) if is_dist else (256.0, {"world": 1})
+        log_rank0(f"Bucket autotune: {bucket_mb} MiB {tune}")
     if is_dist or overlap:
-        reducer = GradReducer(flat, bucket_cap_mb=args.bucket_cap_mb, backend=args.allreduce)
+        reducer = GradReducer(flat, bucket_cap_mb=bucket_mb, backend=args.allreduce)
         log_rank0(f"Gradient buckets: {reducer.num_buckets}, {sum(reducer.bucket_bytes()) / 2**30:.2f} GiB"
                   f"{' (RCCL all-reduce)' if is_dist else ''}")
     model.train()

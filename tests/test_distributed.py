@@ -396,3 +396,54 @@ def test_w4_timeaware_stop_flag_uneven_batch(tmp_path):
     argv2[argv2.index("--batch-size") + 1] = "6"
     mp.spawn(_worker_slurm, args=(4, _free_port(), argv2, str(tmp_path), None), nprocs=4, join=True)
     assert torch.load(tmp_path / "res_0.pt", weights_only=False)["step"] == 3
+
+
+# ---------------------------------------------------------------------------------------------
+# Bucket-size autotune (parallel/bucket_tune.py)
+
+
+def test_bucket_tune_fit_and_choice():
+    from pyrecover_amd.parallel.bucket_tune import choose_bucket_mb, fit_latency_bandwidth, parse_bucket_arg
+
+    mib = 2 ** 20
+    # t = 30 us + s / 150 GB/s, exactly
+    samples = [(s * mib, 30e-6 + s * mib / 150e9) for s in (4, 16, 64, 256)]
+    a, b = fit_latency_bandwidth(samples)
+    assert a == pytest.approx(30e-6, rel=1e-6) and b == pytest.approx(150e9, rel=1e-6)
+    # alpha <= 10% of t(s)  <=>  s >= 9 alpha beta = 40.5 MB = 38.6 MiB -> 64 MiB (powers of two from 16)
+    assert choose_bucket_mb(a, b) == 64
+    assert choose_bucket_mb(1e-3, 150e9) == 512  # clamped at hi
+    assert choose_bucket_mb(0.0, 150e9) == 16 and choose_bucket_mb(1e-5, float("inf")) == 16
+    assert parse_bucket_arg("auto") == "auto" and parse_bucket_arg("32") == 32.0
+    with pytest.raises(ValueError):
+        parse_bucket_arg("-1")
+
+
+def _tune_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    from pyrecover_amd.parallel.bucket_tune import autotune_bucket_mb
+
+    mb, rep = autotune_bucket_mb(torch.device("cpu"), torch.float32, sizes_mb=(1, 2, 4), iters=2)
+    torch.save({"mb": mb, "rep": rep}, os.path.join(out_dir, f"tune_{rank}.pt"))
+    torch.distributed.destroy_process_group()
+
+
+def test_bucket_autotune_two_ranks_agree(tmp_path):
+    """The probe runs on the job's group, every rank ends with rank 0's choice, and the report carries
+    the fitted latency / bandwidth and the per-size times."""
+    mp.spawn(_tune_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    r0, r1 = (torch.load(os.path.join(tmp_path, f"tune_{r}.pt"), weights_only=False) for r in (0, 1))
+    assert r0["mb"] == r1["mb"] and 16 <= r0["mb"] <= 512
+    rep = r0["rep"]
+    assert rep["world"] == 2 and rep["chosen_mb"] == r0["mb"] and len(rep["probe"]) == 3
+    assert all(p["ms"] > 0 for p in rep["probe"])
+
+
+def test_train_bucket_cap_auto_two_ranks(tmp_path):
+    """--bucket-cap-mb auto end to end (train.py, 2 gloo ranks)."""
+    argv = _argv(tmp_path / "ck", 2, ["--distributed"])
+    argv[argv.index("--bucket-cap-mb") + 1] = "auto"
+    res = _run(2, argv, tmp_path)
+    assert res is not None
