@@ -18,7 +18,7 @@ def test_bench_gpus2_spawns_two_ranks(cuda):
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
     env.update(PYRECOVER_LOCAL_DEVICE="0", PYRECOVER_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--model", "gpt2-small",
-                        "--batch-per-gpu", "2", "--steps", "3", "--warmup", "1"],
+                        "--batch-per-gpu", "2", "--steps", "3", "--warmup", "1", "--bucket-mb", "auto"],
                        capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert r.returncode == 0, (r.stdout + r.stderr)[-5000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')]
@@ -34,3 +34,6 @@ def test_bench_gpus2_spawns_two_ranks(cuda):
     assert len(c["buckets"]) == out["config"]["grad_buckets"]
     assert all(b["ms"] >= 0 and b["mib"] > 0 for b in c["buckets"])
     assert "comm_env" in out
+    # --bucket-mb auto: the startup probe ran on the 2-rank group and chose the bucket cap
+    tune = out["config"]["bucket_autotune"]
+    assert tune["world"] == 2 and tune["chosen_mb"] == out["config"]["bucket_mb"] and len(tune["probe"]) == 4
