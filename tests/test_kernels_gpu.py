@@ -196,9 +196,10 @@ def _qkv(cuda, B, S, Hq, Hkv, D, seed=0, scale=1.0):
 @pytest.mark.parametrize("B,S,Hq,Hkv,D", [(1, 256, 4, 4, 128), (2, 512, 8, 2, 128), (1, 384, 4, 1, 64),
                                           (1, 128, 2, 2, 64), (1, 192, 4, 2, 128)])
 @pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("pipe", [0, 1])
+@pytest.mark.parametrize("pipe", [0, 1, 2])
 def test_attention_fwd(cuda, attn_opts, pipe, B, S, Hq, Hkv, D, causal):
-    """Both forward kernels (fwd_pipe: fwd_kernel / cross-tile pipelined fwd_p_kernel)."""
+    """Every forward kernel (fwd_pipe: fwd_kernel / cross-tile pipelined fwd_p_kernel / 16x16x32
+    fwd16_kernel for causal head_dim 128, the pipelined kernel otherwise)."""
     attn_opts(fwd_pipe=pipe)
     C = _ext.native()
     _, q, k, v = _qkv(cuda, B, S, Hq, Hkv, D)
@@ -209,7 +210,7 @@ def test_attention_fwd(cuda, attn_opts, pipe, B, S, Hq, Hkv, D, causal):
     assert (lse - lse_ref).abs().max().item() < 1e-3
 
 
-@pytest.mark.parametrize("pipe", [0, 1])
+@pytest.mark.parametrize("pipe", [0, 1, 2])
 @pytest.mark.parametrize("thr", [0.0, 8.0])
 def test_attention_fwd_rescale_spike(cuda, attn_opts, pipe, thr):
     """Forces the online-softmax running max to jump at a late key tile (rule 26), with the exact

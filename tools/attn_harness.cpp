@@ -72,8 +72,13 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&dk, (size_t)B * S * Hkv * D * 2));
   CK(hipMalloc(&dv, (size_t)B * S * Hkv * D * 2));
   CK(hipMalloc(&lse, (size_t)B * Hq * S * 4));
-  // PRA_BWD_FUSED=0/1: split dQ + dK/dV kernels or the fused backward (default: by shape)
-  if (const char* e = getenv("PRA_BWD_FUSED")) pra_attn_set_options(-1, 8.f, -1, -1, 1, -2, atoi(e), 0);
+  // PRA_BWD_FUSED=0/1: split dQ + dK/dV kernels or the fused backward; PRA_FWD_PIPE=0/1/2: forward
+  // kernel (fwd_kernel / pipelined fwd_p_kernel / 16x16x32 fwd16_kernel); unset = the defaults
+  {
+    const char* f = getenv("PRA_FWD_PIPE");
+    const char* e = getenv("PRA_BWD_FUSED");
+    if (f || e) pra_attn_set_options(f ? atoi(f) : -1, 8.f, -1, -1, 1, -2, e ? atoi(e) : 0, 0);
+  }
   const long nws = pra_attn_bwd_workspace(pra::kBF16, B, S, Hq, Hkv, D);
   CK(hipMalloc(&ws, (size_t)nws * 4));
   CK(hipMemcpy(qkv, h_qkv.data(), nqkv * 2, hipMemcpyHostToDevice));
