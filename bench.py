@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--batch-per-gpu", type=int, default=16)
     ap.add_argument("--bucket-mb", type=_bucket_arg, default=256.0,
                     help="all-reduce bucket MiB, or 'auto' (startup probe: parallel/bucket_tune.py)")
+    ap.add_argument("--master-weights", choices=["none", "fp32"], default="none",
+                    help="fp32 master weights + moments (default none: pure bf16, as the reference)")
     ap.add_argument("--lr", type=float, default=1e-5)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--profile-steps", type=int, default=0, help="emit roctx ranges for this many steps")
@@ -166,7 +168,8 @@ def main():
         args.bucket_mb, bucket_tune = autotune_bucket_mb(dev, flat.grad.dtype)
     reducer = GradReducer(flat, bucket_cap_mb=args.bucket_mb, backend=args.allreduce)
     timer = reducer.enable_comm_timing() if world > 1 and not args.no_comm_timing else None
-    opt = FlatAdamW(flat, lr=args.lr, fused=True, grad_scale=1.0 / world)
+    opt = FlatAdamW(flat, lr=args.lr, fused=True, grad_scale=1.0 / world,
+                    master_weights=args.master_weights == "fp32")
     if not args.no_overlap_optimizer:
         opt.enable_overlap(reducer)
     sched = build_lr_scheduler(opt, 10)
@@ -274,6 +277,7 @@ def main():
                        "seq_len": S, "parallelism": f"dp{world}", "batch_per_gpu": B,
                        "bucket_mb": args.bucket_mb if world > 1 else None,
                        "bucket_autotune": bucket_tune,
+                       "master_weights": args.master_weights,
                        "allreduce": (None if world == 1 else "xgmi" if args.allreduce == "xgmi" else
                                      "rccl" if torch.distributed.get_backend() == "nccl" else
                                      torch.distributed.get_backend()),

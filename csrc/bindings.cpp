@@ -405,6 +405,39 @@ void adamw_flat_(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, 
         "adamw_flat");
 }
 
+// fp32-master AdamW: pm, m, v fp32; p (16-bit) <- round(pm); g has p's dtype.
+void adamw_master_(at::Tensor p, at::Tensor pm, const at::Tensor& g, at::Tensor m, at::Tensor v, double lr, double b1,
+                   double b2, double eps, double wd, double bc1, double bc2_sqrt, double gscale,
+                   const c10::optional<at::Tensor>& gscale_dev, const c10::optional<at::Tensor>& hyper_dev, bool fast) {
+  const Range range_("pyrecover::adamw_master");
+  check_dev(p, "p");
+  TORCH_CHECK(p.is_contiguous() && pm.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous(),
+              "adamw_master: contiguous");
+  TORCH_CHECK(p.numel() == pm.numel() && p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(),
+              "adamw_master: sizes");
+  TORCH_CHECK(p.element_size() == 2 && g.scalar_type() == p.scalar_type(), "adamw_master: 16-bit p and g");
+  TORCH_CHECK(pm.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat,
+              "adamw_master: fp32 master and moments");
+  for (const at::Tensor& t : {pm, g, m, v}) same_dev(p, t, "adamw_master operand");
+  const c10::DeviceGuard guard(p.device());
+  const float* gsd = nullptr;
+  if (gscale_dev.has_value()) {
+    TORCH_CHECK(gscale_dev->scalar_type() == at::kFloat && gscale_dev->numel() >= 1, "adamw_master: gscale_dev fp32");
+    same_dev(p, *gscale_dev, "gscale_dev");
+    gsd = gscale_dev->data_ptr<float>();
+  }
+  const double* hyd = nullptr;
+  if (hyper_dev.has_value()) {
+    TORCH_CHECK(hyper_dev->scalar_type() == at::kDouble && hyper_dev->numel() >= 3, "adamw_master: hyper_dev fp64[3]");
+    same_dev(p, *hyper_dev, "hyper_dev");
+    hyd = hyper_dev->data_ptr<double>();
+  }
+  check(pra_adamw_master(dt(p), p.data_ptr(), pm.data_ptr<float>(), g.data_ptr(), m.data_ptr<float>(),
+                         v.data_ptr<float>(), p.numel(), lr, b1, b2, eps, wd, bc1, bc2_sqrt, (float)gscale, gsd, hyd,
+                         fast ? 1 : 0, stream_of(p)),
+        "adamw_master");
+}
+
 // AdamW of one row-major weight matrix p [rows, cols] that also writes pt = p^T [cols, rows].
 void adamw_t_(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, at::Tensor pt, double lr, double b1,
               double b2, double eps, double wd, double bc1, double bc2_sqrt, double gscale,
@@ -774,6 +807,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("fast") = false);
   m.def("adamw_t_", &adamw_t_, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("pt"), py::arg("lr"),
         py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("bc1"), py::arg("bc2_sqrt"),
+        py::arg("gscale"), py::arg("gscale_dev") = py::none(), py::arg("hyper_dev") = py::none(),
+        py::arg("fast") = false);
+  m.def("adamw_master_", &adamw_master_, py::arg("p"), py::arg("pm"), py::arg("g"), py::arg("m"), py::arg("v"),
+        py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("bc1"), py::arg("bc2_sqrt"),
         py::arg("gscale"), py::arg("gscale_dev") = py::none(), py::arg("hyper_dev") = py::none(),
         py::arg("fast") = false);
   m.def("grad_norm", &grad_norm);

@@ -65,6 +65,10 @@ hipError_t pra_xent_bwd(int dtype, void* logits, const int64_t* labels, const fl
 hipError_t pra_adamw_flat(int pdtype, int sdtype, void* p, const void* g, void* m, void* v, long n, double lr,
                           double b1, double b2, double eps, double wd, double bc1, double bc2_sqrt, float gscale,
                           const float* gscale_dev, const double* hyper_dev, int fast, hipStream_t s);
+// fp32-master AdamW: updates pm / m / v (fp32) and writes p = round(pm) (16-bit params)
+hipError_t pra_adamw_master(int pdtype, void* p, float* pm, const void* g, float* m, float* v, long n, double lr,
+                            double b1, double b2, double eps, double wd, double bc1, double bc2_sqrt, float gscale,
+                            const float* gscale_dev, const double* hyper_dev, int fast, hipStream_t s);
 int pra_sumsq_partials();
 hipError_t pra_grad_norm(int dtype, const void* x, long n, float* ws, float* out, float max_norm, float pre_scale,
                          hipStream_t s);

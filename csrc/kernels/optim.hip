@@ -113,6 +113,44 @@ __global__ __launch_bounds__(256) void adamw_kernel(P* __restrict__ p, const P* 
   }
 }
 
+// AdamW with fp32 master weights (--master-weights fp32): the update runs on the fp32
+// master pm and fp32 moments (same adamw_elem math), and the 16-bit model parameter p the forward
+// reads is pm rounded once. g is the 16-bit gradient.
+template <typename P, bool FAST>
+__global__ __launch_bounds__(256) void adamw_master_kernel(P* __restrict__ p, float* __restrict__ pm,
+                                                           const P* __restrict__ g, float* __restrict__ m,
+                                                           float* __restrict__ v, long n, double lr, double b1,
+                                                           double b2, double eps, double wd, double bc1,
+                                                           double bc2_sqrt, float gscale,
+                                                           const float* __restrict__ gscale_dev,
+                                                           const double* __restrict__ hyper_dev) {
+  const float gs = gscale_dev ? gscale * gscale_dev[0] : gscale;
+  const AdamCoef c = adam_coef(lr, b1, b2, eps, wd, bc1, bc2_sqrt, hyper_dev);
+  const long n8 = n / 8;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    const long o = i * 8;
+    float pv[8], gv[8], mv[8], vv[8];
+    load8<float>(pm + o, pv);
+    load8<P>(g + o, gv);
+    load8<float>(m + o, mv);
+    load8<float>(v + o, vv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) adamw_elem<FAST>(pv[j], mv[j], vv[j], gv[j], gs, c);
+    store8<float>(pm + o, pv);
+    store8<float>(m + o, mv);
+    store8<float>(v + o, vv);
+    store8<P>(p + o, pv);
+  }
+  for (long o = n8 * 8 + (long)blockIdx.x * 256 + threadIdx.x; o < n; o += (long)gridDim.x * 256) {
+    float pv = pm[o], mv = m[o], vv = v[o];
+    adamw_elem<FAST>(pv, mv, vv, to_f<P>(g[o]), gs, c);
+    pm[o] = pv;
+    m[o] = mv;
+    v[o] = vv;
+    p[o] = from_f<P>(pv);
+  }
+}
+
 // AdamW over one row-major [rows, cols] weight matrix that ALSO writes its transposed copy
 // pt [cols, rows] (the data-gradient GEMM's operand, parallel/flat.py "weight shadows") from the
 // updated values it already holds: the separate transpose pass re-read the whole model after
@@ -238,6 +276,26 @@ hipError_t pra_adamw_t(int dtype, void* p, const void* g, void* m, void* v, void
                        hipLaunchKernelGGL((pra::adamw_t_kernel<T, false>), grid, dim3(256), 0, s, (T*)p, (const T*)g,
                                           (T*)m, (T*)v, (T*)pt, rows, cols, lr, b1, b2, eps, wd, bc1, bc2_sqrt,
                                           gscale, gscale_dev, hyper_dev));
+  }
+  return hipGetLastError();
+}
+
+hipError_t pra_adamw_master(int pdtype, void* p, float* pm, const void* g, float* m, float* v, long n, double lr,
+                            double b1, double b2, double eps, double wd, double bc1, double bc2_sqrt, float gscale,
+                            const float* gscale_dev, const double* hyper_dev, int fast, hipStream_t s) {
+  long blocks = (n / 8 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  if (fast) {
+    PRA_DISPATCH_16BIT(pdtype, T,
+                       hipLaunchKernelGGL((pra::adamw_master_kernel<T, true>), dim3(blocks), dim3(256), 0, s, (T*)p,
+                                          pm, (const T*)g, m, v, n, lr, b1, b2, eps, wd, bc1, bc2_sqrt, gscale,
+                                          gscale_dev, hyper_dev));
+  } else {
+    PRA_DISPATCH_16BIT(pdtype, T,
+                       hipLaunchKernelGGL((pra::adamw_master_kernel<T, false>), dim3(blocks), dim3(256), 0, s, (T*)p,
+                                          pm, (const T*)g, m, v, n, lr, b1, b2, eps, wd, bc1, bc2_sqrt, gscale,
+                                          gscale_dev, hyper_dev));
   }
   return hipGetLastError();
 }

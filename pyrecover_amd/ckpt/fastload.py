@@ -140,7 +140,18 @@ def flat_buffers(model, optimizer) -> List[torch.Tensor]:
         out.append(flat.data)
     if optimizer is not None and _opt_targets(optimizer) is not None:
         out += [optimizer.exp_avg, optimizer.exp_avg_sq]
+        if getattr(optimizer, "master", None) is not None:
+            out.append(optimizer.master)
     return out
+
+
+def _opt_keys(mine: Dict[str, torch.Tensor], saved: Optional[Dict[str, Any]] = None) -> Tuple[str, ...]:
+    """Per-parameter optimizer tensors to place: the moments, plus the fp32 master when this run keeps
+    one and the checkpoint has it (FlatAdamW master_weights)."""
+    keys = ("exp_avg", "exp_avg_sq")
+    if "master_param" in mine and (saved is None or "master_param" in saved):
+        keys += ("master_param",)
+    return keys
 
 
 # ------------------------------------------------------------------------------------------
@@ -183,7 +194,7 @@ def plan_vanilla(path: str, model, optimizer) -> Tuple[Dict[str, Any], Plan]:
         sids = osd["param_groups"][0]["params"]
         if len(sids) == len(ot) and all(sid in osd["state"] for sid in sids):
             for sid, mine in zip(sids, ot):
-                for key in ("exp_avg", "exp_avg_sq"):
+                for key in _opt_keys(mine, osd["state"][sid]):
                     place(osd["state"][sid][key], mine[key])
             plan.opt_tensors = True
     return ckpt, plan
@@ -349,7 +360,8 @@ def plan_sharded(path: str, model, optimizer) -> Tuple[Dict[str, Any], Plan]:
         raise ValueError("no manifest (not written by pyrecover_amd)")
     manifest = json.loads(mf.read_text())
     native = {k: e for k, e in manifest.items() if "data_offset" in e and
-              (k.startswith("model.") or (k.startswith("optimizer.state.") and k.endswith((".exp_avg", ".exp_avg_sq"))))}
+              (k.startswith("model.") or (k.startswith("optimizer.state.") and
+                                          k.endswith((".exp_avg", ".exp_avg_sq", ".master_param"))))}
     ckpt = sharded.build_ckpt(sharded.read_sharded_state(path, skip=set(native)))
     plan = Plan()
     tg = _model_targets(model)
@@ -377,7 +389,7 @@ def plan_sharded(path: str, model, optimizer) -> Tuple[Dict[str, Any], Plan]:
     if ot is not None and osd is not None and osd.get("param_groups"):
         sids = osd["param_groups"][0]["params"]
         fq = [(f"optimizer.state.{sid}.{key}", mine[key]) for sid, mine in zip(sids, ot)
-              for key in ("exp_avg", "exp_avg_sq")]
+              for key in _opt_keys(mine)]
         if len(sids) == len(ot) and all(f in native for f, _ in fq):
             for f, dst in fq:
                 if place(f, dst):

@@ -55,6 +55,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--batch-size", type=int, default=1,
                    help="GLOBAL batch size; each rank uses max(batch_size // world_size, 1) (reference semantics)")
     p.add_argument("--fused-optimizer", action="store_true")
+    p.add_argument("--master-weights", choices=["none", "fp32"], default="none",
+                   help="fp32: AdamW updates an fp32 master copy with fp32 moments and the 16-bit model "
+                        "parameters are the master rounded (default none: pure-dtype training, as the reference)")
     p.add_argument("--learning-rate", type=float, default=1e-5)
     p.add_argument("--lr-warmup-steps", type=int, default=10)
     p.add_argument("--training-steps", type=int, default=1000)

@@ -6,6 +6,13 @@ The reference builds ``torch.optim.AdamW(model.parameters(), lr, fused=--fused-o
 ``state[i] = {"step", "exp_avg", "exp_avg_sq"}`` in ``model.parameters()`` order), but the moments
 live in two flat buffers laid out like the flat parameters, and the update is one HIP kernel
 over the whole model (``pra_adamw_flat``: fp32 opmath, torch ``_fused_adamw_`` semantics).
+
+``master_weights=True`` (``--master-weights fp32``; SURVEY §8 D18: "keep pure-bf16 as the default for
+parity, optional fp32 master"): the update runs on an fp32 master copy of the parameters with fp32
+moments (``pra_adamw_master``), and the 16-bit parameters the model computes with are the master
+rounded once after every update. The master is saved as a third per-parameter state tensor
+(``state[i]["master_param"]``) next to the fp32 moments; a checkpoint without it (pure-bf16 runs,
+the reference's) resumes with the master taken from the loaded parameters.
 """
 from __future__ import annotations
 
@@ -47,7 +54,8 @@ FAST_MATH = os.environ.get("PYRECOVER_ADAMW_FAST", "0") == "1"
 
 class FlatAdamW(torch.optim.AdamW):
     def __init__(self, flat: FlatParams, params=None, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 1e-2, fused: Optional[bool] = None, grad_scale: float = 1.0):
+                 weight_decay: float = 1e-2, fused: Optional[bool] = None, grad_scale: float = 1.0,
+                 master_weights: bool = False):
         # default order = the model's parameters() order when the model recorded it (the
         # reference's optimizer-state indices), else the flat buffer order
         params = list(params) if params is not None else list(getattr(flat, "module_order", None) or flat.params)
@@ -64,8 +72,13 @@ class FlatAdamW(torch.optim.AdamW):
         self.flat = flat
         self.grad_scale = grad_scale  # e.g. 1/world_size after a SUM all-reduce
         self.grad_scale_dev: Optional[torch.Tensor] = None  # device-side multiplier (clipping)
-        self.exp_avg = torch.zeros_like(flat.data)
-        self.exp_avg_sq = torch.zeros_like(flat.data)
+        # fp32 master + fp32 moments for 16-bit parameters (fp32 / fp64 models already update in place)
+        self.master: Optional[torch.Tensor] = None
+        if master_weights and flat.data.element_size() == 2:
+            self.master = flat.data.float()
+        sdt = torch.float32 if self.master is not None else flat.data.dtype
+        self.exp_avg = torch.zeros(flat.data.shape, dtype=sdt, device=flat.data.device)
+        self.exp_avg_sq = torch.zeros(flat.data.shape, dtype=sdt, device=flat.data.device)
         self._step = 0
         self._bind_state()
         self.overlap = False
@@ -132,6 +145,12 @@ class FlatAdamW(torch.optim.AdamW):
         m, v = self.exp_avg, self.exp_avg_sq
 
         fast = FAST_MATH
+        if self.master is not None:
+            # fp32 master update, then the transposed shadows of the matrices in range from the
+            # rounded parameters (same stream: the next backward sees them)
+            C.adamw_master_(f.data[lo:hi], self.master[lo:hi], f.grad[lo:hi], m[lo:hi], v[lo:hi], *args, fast)
+            f.refresh_transposed(lo, hi)
+            return
 
         def flat_update(a, b):
             if a < b:
@@ -205,9 +224,11 @@ class FlatAdamW(torch.optim.AdamW):
             n = p.numel()
             self.state[p] = {
                 "step": torch.tensor(float(self._step), dtype=torch.float32),
-                "exp_avg": self.exp_avg[o:o + n].view_as(p),
-                "exp_avg_sq": self.exp_avg_sq[o:o + n].view_as(p),
+                "exp_avg": self.exp_avg[o:o + n].view(p.shape),
+                "exp_avg_sq": self.exp_avg_sq[o:o + n].view(p.shape),
             }
+            if self.master is not None:
+                self.state[p]["master_param"] = self.master[o:o + n].view(p.shape)
 
     # --- torch.optim.Optimizer API ------------------------------------------------------
     def zero_grad(self, set_to_none: bool = True):
@@ -252,7 +273,7 @@ class FlatAdamW(torch.optim.AdamW):
         # weights other layers saved for their backward (the HIP kernels write through pointers)
         pd, gd, md, vd = f.data.data[lo:hi], f.grad[lo:hi], self.exp_avg[lo:hi], self.exp_avg_sq[lo:hi]
         ct = torch.promote_types(pd.dtype, torch.float32)  # fp32 opmath; fp64 models stay fp64
-        p = pd.to(ct)
+        p = (self.master[lo:hi] if self.master is not None else pd).to(ct)
         gr = gd.to(ct) * gs
         m = md.to(ct)
         v = vd.to(ct)
@@ -261,6 +282,8 @@ class FlatAdamW(torch.optim.AdamW):
         v.mul_(b2).addcmul_(gr, gr, value=1 - b2)
         denom = v.sqrt().div_(bc2_sqrt).add_(eps)
         p.addcdiv_(m, denom, value=-(lr / bc1))
+        if self.master is not None:
+            self.master[lo:hi].copy_(p)
         pd.copy_(p)
         md.copy_(m)
         vd.copy_(v)
@@ -290,6 +313,11 @@ class FlatAdamW(torch.optim.AdamW):
             for sid, p in zip(saved_ids, params):
                 st = state_dict["state"].get(sid, state_dict["state"].get(str(sid)))
                 mine = self.state[p]
+                if "master_param" in mine and (st is None or "master_param" not in st or not tensors_loaded):
+                    # a checkpoint without a master (pure-bf16 run, the reference's): take the loaded
+                    # parameters; with one, its fp32 values
+                    src = st.get("master_param") if st is not None else None
+                    mine["master_param"].copy_(src if src is not None else p.detach())
                 if st is None:
                     if not tensors_loaded:
                         mine["exp_avg"].zero_()

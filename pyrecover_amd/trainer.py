@@ -237,7 +237,11 @@ def train(args):
     model.train()
     # SUM all-reduce of `accum` summed micro-batch gradients: the mean is folded into the update
     grad_scale = 1.0 / (world_size * accum)
-    optimizer = FlatAdamW(flat, lr=args.learning_rate, fused=args.fused_optimizer, grad_scale=grad_scale)
+    optimizer = FlatAdamW(flat, lr=args.learning_rate, fused=args.fused_optimizer, grad_scale=grad_scale,
+                          master_weights=getattr(args, "master_weights", "none") == "fp32")
+    if optimizer.master is not None:
+        log_rank0(f"fp32 master weights: {optimizer.master.numel() * 4 / 2**30:.2f} GiB "
+                  f"(+ fp32 moments {2 * optimizer.exp_avg.numel() * 4 / 2**30:.2f} GiB)")
     if overlap:
         optimizer.enable_overlap(reducer)
         optimizer.pre_update_fences.append(ckcore.fence_all)

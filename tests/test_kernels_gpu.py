@@ -174,6 +174,30 @@ def test_adamw_matches_torch_fused(cuda, fast, dtype):
     assert _rel(p, p2) < 1e-2 and _rel(m, m2) < 1e-2 and _rel(v, v2) < 1e-2
 
 
+@pytest.mark.parametrize("n", [(1 << 22) + 5, 1000])
+def test_adamw_master_matches_fp32_torch_fused(cuda, n):
+    """--master-weights fp32: the fp32 master, m and v are bit-equal to torch's fused AdamW run in fp32
+    on the widened bf16 gradient, and the bf16 parameter is the master rounded to nearest even (the
+    odd n exercises the scalar tail)."""
+    C = _ext.native()
+    torch.manual_seed(2)
+    pm = torch.randn(n, device=cuda)
+    p = pm.to(torch.bfloat16)
+    m = torch.zeros_like(pm)
+    v = torch.zeros_like(pm)
+    p2, m2, v2 = pm.clone(), m.clone(), v.clone()
+    step = torch.zeros((), device=cuda)
+    lr, b1, b2, eps, wd = 1e-3, 0.9, 0.95, 1e-8, 0.1
+    for s in range(1, 4):
+        g = (torch.randn(n, device=cuda) * 10.0 ** (-s)).to(torch.bfloat16)
+        C.adamw_master_(p, pm, g, m, v, lr, b1, b2, eps, wd, 1 - b1 ** s, math.sqrt(1 - b2 ** s), 1.0)
+        step += 1
+        torch._fused_adamw_([p2], [g.float()], [m2], [v2], [], [step], amsgrad=False, lr=lr, beta1=b1, beta2=b2,
+                            weight_decay=wd, eps=eps, maximize=False)
+    assert torch.equal(pm, p2) and torch.equal(m, m2) and torch.equal(v, v2)
+    assert torch.equal(p, p2.to(torch.bfloat16))
+
+
 def test_grad_norm(cuda):
     C = _ext.native()
     x = torch.randn(3_000_001, device=cuda, dtype=torch.bfloat16)

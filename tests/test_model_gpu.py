@@ -284,10 +284,11 @@ def test_weight_shadows_off_gives_the_same_gradients(cuda, monkeypatch):
     assert rel < 1e-2, rel
 
 
-@pytest.mark.parametrize("dtype", ["fp16", "fp32", "fp64"])
+@pytest.mark.parametrize("dtype", ["fp16", "fp32", "fp64", "bf16+master"])
 def test_train_py_model_dtypes(cuda, tmp_path, dtype):
     """train.py --model-dtype {fp16,fp32,fp64} on the GPU: a few steps, finite loss, a checkpoint
-    that resumes (reference utils.py:176-181, train.py:100-101)."""
+    that resumes (reference utils.py:176-181, train.py:100-101); bf16+master adds the fp32 master
+    weights (--master-weights fp32, adamw_master kernel)."""
     import os
     import subprocess
     import sys
@@ -295,8 +296,10 @@ def test_train_py_model_dtypes(cuda, tmp_path, dtype):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     args = [sys.executable, os.path.join(root, "train.py"), "--model-preset", "llama-tiny", "--synthetic-data",
             "--batch-size", "2", "--sequence-length", "200", "--training-steps", "4", "--checkpoint-frequency", "2",
-            "--logging-frequency", "1", "--num-workers", "0", "--model-dtype", dtype,
+            "--logging-frequency", "1", "--num-workers", "0", "--model-dtype", dtype.split("+")[0],
             "--checkpoint-dir", str(tmp_path), "--experiment_name", "dt"]
+    if dtype.endswith("+master"):
+        args += ["--master-weights", "fp32"]
     r = subprocess.run(args, capture_output=True, text=True, timeout=300, cwd=root)
     assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
     assert "Loss: nan" not in r.stdout + r.stderr

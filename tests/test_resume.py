@@ -280,3 +280,44 @@ def test_async_sharded_checkpoint_survives_poll_and_next_save(tmp_path):
     assert s == 10
     for k, v in fresh.state_dict().items():
         assert torch.equal(v, snap[k]), k
+
+
+@pytest.mark.parametrize("sharded", [False, True])
+def test_resume_bit_exact_fp32_master_weights(tmp_path, sharded):
+    """--master-weights fp32 (optional): bf16 model, fp32 master and moments; the master
+    is checkpointed next to the moments and a resumed run is bit-identical, master included."""
+    extra = ["--model-dtype", "bf16", "--master-weights", "fp32"]
+    straight = tmp_path / "a"
+    train(_args(straight, 6, extra, sharded=sharded))
+    split = tmp_path / "b"
+    r = train(_args(split, 6, extra + ["--stop-at-step", "4"], sharded=sharded))
+    assert r["stopped_early"] and r["step"] == 4
+    train(_args(split, 6, extra, sharded=sharded, resume="latest"))
+    name = "ckpt_6" if sharded else "ckpt_6.pt"
+    a = _load_final(str(straight / "exp" / name), sharded)
+    b = _load_final(str(split / "exp" / name), sharded)
+    _assert_same(a, b)
+    sa_, sb_ = a[1]["state"], b[1]["state"]
+    for k in sa_:
+        kb = k if k in sb_ else str(k)
+        ma, mb = sa_[k]["master_param"], sb_[kb]["master_param"]
+        assert ma.dtype == torch.float32 and torch.equal(ma, mb), k
+        assert sa_[k]["exp_avg"].dtype == torch.float32
+    # the model's bf16 parameters are the master rounded
+    sid = next(iter(sa_))
+    assert any(torch.equal(v.float(), sa_[sid]["master_param"].to(torch.bfloat16).float())
+               for v in a[0].values() if v.shape == sa_[sid]["master_param"].shape)
+
+
+def test_fp32_master_resumes_from_pure_bf16_checkpoint(tmp_path):
+    """A pure-bf16 checkpoint (no master in the optimizer state, e.g. the reference's) resumed with
+    --master-weights fp32: the master starts from the loaded parameters, the moments are widened."""
+    ck = tmp_path / "c"
+    train(_args(ck, 3, ["--model-dtype", "bf16"]))
+    st3 = torch.load(str(ck / "exp" / "ckpt_3.pt"), weights_only=True)["optimizer"]["state"]
+    assert all("master_param" not in v for v in st3.values())
+    r = train(_args(ck, 6, ["--model-dtype", "bf16", "--master-weights", "fp32"], resume="latest"))
+    assert r["step"] == 6
+    st6 = torch.load(str(ck / "exp" / "ckpt_6.pt"), weights_only=True)["optimizer"]["state"]
+    for v in st6.values():
+        assert v["master_param"].dtype == torch.float32 and v["exp_avg"].dtype == torch.float32
