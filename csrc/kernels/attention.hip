@@ -48,6 +48,27 @@
 namespace pra {
 namespace attn {
 
+// Block -> (query tile, batch * head) of the forward / dQ grids (nqt * BH blocks).
+// grp = 0: heavy (late) query tiles first across the whole grid, consecutive blocks on different
+// heads. grp = G > 0 (host: BH % 8 == 0 and (BH / 8) % G == 0): XCD-grouped. Workgroups are
+// dispatched to the 8 XCDs round-robin (block i on XCD i % 8), so XCD x walks its own contiguous
+// range of BH / 8 heads, G heads at a time with all their query tiles (heaviest first): the query
+// tiles of a head run together on one XCD and read its K/V tiles from HBM once, the other tiles
+// hitting that XCD's L2 (grp 0 re-reads every head's K/V from HBM once per query tile at MHA).
+// Adjacent heads (one GQA group) share an XCD.
+__device__ __forceinline__ void block_tile(int nqt, int BH, int grp, int& qt, int& bh) {
+  const int i = blockIdx.x;
+  if (grp <= 0) {
+    qt = nqt - 1 - i / BH;
+    bh = i % BH;
+    return;
+  }
+  const int x = i & 7, j = i >> 3, per = BH >> 3, span = grp * nqt;
+  const int g = j / span, r = j - g * span;
+  qt = nqt - 1 - r / grp;
+  bh = x * per + g * grp + r % grp;
+}
+
 
 // ======================================================================================
 // Forward
@@ -408,7 +429,8 @@ template <typename T, int D, bool CAUSAL, int NW>
 __global__ __launch_bounds__(NW * 64, PRA_FWD_MINBLK) void fwd_p_kernel(const T* __restrict__ Q, const T* __restrict__ K,
                                                            const T* __restrict__ V, T* __restrict__ O,
                                                            float* __restrict__ LSE, int S, int Hq, int Hkv, long ldq,
-                                                           long ldk, long ldv, long ldo, float scale_log2, float thr) {
+                                                           long ldk, long ldv, long ldo, float scale_log2, float thr,
+                                                           int grp) {
   constexpr int KT = 64, QT = 32 * NW;
   constexpr int NKS = D / 16, NDB = D / 32, TILE = KT * D;
   // (K V) x 3, one __shared__ object per ring slot: the LDS lowering gives each object its own alias
@@ -422,8 +444,8 @@ __global__ __launch_bounds__(NW * 64, PRA_FWD_MINBLK) void fwd_p_kernel(const T*
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h2 = lane >> 5, l32 = lane & 31;
   const int nqt = (S + QT - 1) / QT;
   const int BH = gridDim.x / nqt;
-  const int qt = nqt - 1 - (int)(blockIdx.x / BH);  // heavy (late) query tiles first
-  const int bh = blockIdx.x % BH;
+  int qt, bh;
+  block_tile(nqt, BH, grp, qt, bh);
   const int hq = bh % Hq, b = bh / Hq;
   const int hk = hq / (Hq / Hkv);
   const int q0 = qt * QT, qw = q0 + wid * 32;
@@ -680,7 +702,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
     const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V,
     const T* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
     T* __restrict__ dK, T* __restrict__ dV, int S, int Hq, int Hkv, long ldq, long ldk, long ldv,
-    long lddo, long lddk, long lddv, float scale, float scale_log2, int skv, const float2* __restrict__ rtab) {
+    long lddo, long lddk, long lddv, float scale, float scale_log2, int skv, const float2* __restrict__ rtab,
+    int grp) {
   constexpr int KB = 32 * NW, QT = 32, NT = NW * 64;
   constexpr int NKS = D / 16, NDB = D / 32;
   constexpr int KVT = KB * D, QDT = QT * D;
@@ -696,8 +719,9 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h2 = lane >> 5, l32 = lane & 31;
   const int nkb = S / KB;
   const int BH = gridDim.x / nkb;
-  const int kbk = (int)(blockIdx.x / BH);  // causal: early key tiles have the most work
-  const int bh = blockIdx.x % BH;
+  int kbk, bh;
+  block_tile(nkb, BH, grp, kbk, bh);
+  kbk = nkb - 1 - kbk;  // causal: early key tiles have the most work
   const int hk = bh % Hkv, b = bh / Hkv;
   const int nrep = Hq / Hkv;
   const int k0 = kbk * KB, kw = k0 + wid * 32;
@@ -880,7 +904,7 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_r_kernel(
     const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V, const T* __restrict__ dO,
     const float* __restrict__ RC, long nrc, T* __restrict__ dK, T* __restrict__ dV, int S, int Hq, int Hkv,
     long ldq, long ldk, long ldv, long lddo, long lddk, long lddv, float scale, float scale_log2, int skv,
-    const float2* __restrict__ rtab) {
+    const float2* __restrict__ rtab, int grp) {
   constexpr int NW = 8, KB = 32 * NW, QT = 32;
   constexpr int NKS = D / 16, NDB = D / 32;
   constexpr int KVT = KB * D, QDT = QT * D;
@@ -895,8 +919,9 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_r_kernel(
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h2 = lane >> 5, l32 = lane & 31;
   const int nkb = S / KB;
   const int BH = gridDim.x / nkb;
-  const int kbk = (int)(blockIdx.x / BH);  // causal: early key tiles have the most work
-  const int bh = blockIdx.x % BH;
+  int kbk, bh;
+  block_tile(nkb, BH, grp, kbk, bh);
+  kbk = nkb - 1 - kbk;  // causal: early key tiles have the most work
   const int hk = bh % Hkv, b = bh / Hkv;
   const int nrep = Hq / Hkv;
   const int k0 = kbk * KB, kw = k0 + wid * 32;
@@ -1263,7 +1288,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
     const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V,
     const T* __restrict__ dO, const T* __restrict__ O, const float* __restrict__ LSE, float* __restrict__ Delta,
     T* __restrict__ dQ, int S, int Hq, int Hkv, long ldq, long ldk, long ldv, long lddo, long ldo, long lddq,
-    float scale, float scale_log2, int skv, const float2* __restrict__ rtab, float* __restrict__ RC2, long nrc) {
+    float scale, float scale_log2, int skv, const float2* __restrict__ rtab, float* __restrict__ RC2, long nrc,
+    int grp) {
   constexpr int KT = 64, QT = 32 * NW;
   constexpr int NKS = D / 16, NDB = D / 32, TILE = KT * D;
   // K0 V0 | K1 V1: one __shared__ object per buffer, so the reads of one buffer do not wait
@@ -1274,8 +1300,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h2 = lane >> 5, l32 = lane & 31;
   const int nqt = (S + QT - 1) / QT;
   const int BH = gridDim.x / nqt;
-  const int qt = nqt - 1 - (int)(blockIdx.x / BH);
-  const int bh = blockIdx.x % BH;
+  int qt, bh;
+  block_tile(nqt, BH, grp, qt, bh);
   const int hq = bh % Hq, b = bh / Hq;
   const int hk = hq / (Hq / Hkv);
   const int q0 = qt * QT, qw = q0 + wid * 32;
@@ -1548,8 +1574,26 @@ struct AttnOptions {
   // where the side-stream window (mid_event) opens in the split backward: 0 = between the dQ and the
   // dK/dV kernels (default), 1 = before the dQ kernel (the update then runs beside both)
   int bwd_window = 0;
+  // block order of the pipelined forward (block_tile): 0 = heavy query tiles first across the grid,
+  // G > 0 = XCD-grouped, G heads per group; -1 = by shape (attn_grp)
+  int fwd_order = 0;
+  int dq_order = 0;    // the same for the dQ kernel
+  int dkdv_order = 0;  // and the two-wave / ring dK/dV kernels (key tiles, lightest last)
 };
 AttnOptions g_attn_opts;
+
+// Heads per XCD group for an nqt x BH grid under option `order`, 0 when the grid does not split.
+// By shape (order < 0): at least the rep = Hq / Hkv query heads that share a kv head (forward and dQ
+// grids; 1 for the dK/dV grids, whose heads are kv heads), and at least 32 blocks (one per CU of
+// an XCD) per group. B16 S2048 H32 D128 causal (harness, profiles/r5/attn_order/): forward
+// 0.740 -> 0.650 ms, dQ + dK/dV 2.31 -> 2.11 ms; B1 S8192 H32/8 forward 0.508 -> 0.499 ms.
+static int attn_grp(int order, int nqt, int BH, int rep) {
+  if (order == 0 || BH % 8) return 0;
+  int g = order > 0 ? order : 1;
+  if (order < 0)
+    while ((g * 2 <= rep || g * 2 * nqt <= 32) && (BH / 8) % (g * 2) == 0) g *= 2;
+  return (BH / 8) % g == 0 ? g : 0;
+}
 
 // All tensors bf16 or fp16 (T), layout [B, S, H, D] with token stride ld* (elements); LSE/Delta fp32 [B, Hq, S].
 template <typename T>
@@ -1565,6 +1609,7 @@ hipError_t attn_fwd_t(const void* q, const void* k, const void* v, void* o, floa
   const AttnOptions& op = g_attn_opts;
   const bool pipe = (causal || skv >= S) && (op.fwd_pipe >= 0 ? op.fwd_pipe != 0 : (causal != 0));
   const float thr = op.fwd_thr;
+  const int grp = attn_grp(op.fwd_order, nqt, Hq * B, Hq / Hkv);
   if (op.fwd_pipe == 2 && causal && D == 128) {  // 16x16x32 forward (causal, head_dim 128)
     // (4-wave blocks, two per CU, measured 0.973 ms: the register-staged K/V tile then takes 32 VGPRs)
     hipLaunchKernelGGL((fwd16_kernel<T, NW>), grid, block, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o,
@@ -1574,7 +1619,7 @@ hipError_t attn_fwd_t(const void* q, const void* k, const void* v, void* o, floa
 #define LAUNCH(DD, CC)                                                                                        \
   if (pipe)                                                                                                   \
     hipLaunchKernelGGL((fwd_p_kernel<T, DD, CC, NW>), grid, block, 0, st, (const T*)q, (const T*)k,         \
-                       (const T*)v, (T*)o, lse, S, Hq, Hkv, ldq, ldk, ldv, ldo, sl2, thr);                  \
+                       (const T*)v, (T*)o, lse, S, Hq, Hkv, ldq, ldk, ldv, ldo, sl2, thr, grp);             \
   else                                                                                                        \
     hipLaunchKernelGGL((fwd_kernel<T, DD, CC, NW>), grid, block, 0, st, (const T*)q, (const T*)k,           \
                        (const T*)v, (T*)o, lse, S, Hq, Hkv, ldq, ldk, ldv, ldo, sl2, skv)
@@ -1683,20 +1728,24 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
                     nw == 8 && D == 128;  // bwd_dkdv_r_kernel
   float* rc2 = (p2 || ring) ? delta + nrc : nullptr;
   // dQ first: it also computes delta = rowsum(dO * O), which the dK/dV kernel reads
-  if (mid_event != nullptr && g_attn_opts.bwd_window == 1) hipEventRecord(mid_event, st);
+  if (mid_event != nullptr && g_attn_opts.bwd_window == 1) {
+    const hipError_t e = hipEventRecord(mid_event, st);
+    if (e != hipSuccess) return e;
+  }
   {
     dim3 grid((S / (32 * nw)) * Hq * B);
     // the pipelined kernel has no key bound: padded non-causal sequences take the plain one
     const bool pipe = (causal || skv >= S) && g_attn_opts.dq_pipe != 0;
+    const int gq = attn_grp(g_attn_opts.dq_order, S / (32 * nw), Hq * B, Hq / Hkv);
 #define LAUNCH(DD, CC, NWW)                                                                                     \
   if (pipe)                                                                                                     \
     hipLaunchKernelGGL((bwd_dq_kernel<T, DD, CC, NWW, true>), grid, dim3(NWW * 64), 0, st, (const T*)q,       \
                        (const T*)k, (const T*)v, (const T*)dout, (const T*)o, lse, delta, (T*)dq, S, Hq, Hkv,  \
-                       ldq, ldk, ldv, lddo, ldo, lddq, scale, sl2, skv, rt, rc2, nrc);                              \
+                       ldq, ldk, ldv, lddo, ldo, lddq, scale, sl2, skv, rt, rc2, nrc, gq);                          \
   else                                                                                                          \
     hipLaunchKernelGGL((bwd_dq_kernel<T, DD, CC, NWW>), grid, dim3(NWW * 64), 0, st, (const T*)q,             \
                        (const T*)k, (const T*)v, (const T*)dout, (const T*)o, lse, delta, (T*)dq, S, Hq, Hkv,  \
-                       ldq, ldk, ldv, lddo, ldo, lddq, scale, sl2, skv, rt, rc2, nrc)
+                       ldq, ldk, ldv, lddo, ldo, lddq, scale, sl2, skv, rt, rc2, nrc, gq)
     if (nw == 8) {
       if (D == 128) { if (causal) LAUNCH(128, true, 8); else LAUNCH(128, false, 8); }
       else { if (causal) LAUNCH(64, true, 8); else LAUNCH(64, false, 8); }
@@ -1706,7 +1755,10 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
     }
 #undef LAUNCH
   }
-  if (mid_event != nullptr && g_attn_opts.bwd_window != 1) hipEventRecord(mid_event, st);  // between dQ and dK/dV
+  if (mid_event != nullptr && g_attn_opts.bwd_window != 1) {  // between dQ and dK/dV
+    const hipError_t e = hipEventRecord(mid_event, st);
+    if (e != hipSuccess) return e;
+  }
   const bool window = mid_event != nullptr;
   if (p2) {
     const int ns = window && g_attn_opts.dkdv_split < 0 ? 1 : dkdv_split(B, S, Hq, Hkv, D);
@@ -1729,7 +1781,8 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
 #define LAUNCHR(DD, CC)                                                                                       \
   hipLaunchKernelGGL((bwd_dkdv_r_kernel<T, DD, CC>), grid, dim3(512), 0, st, (const T*)q, (const T*)k,        \
                      (const T*)v, (const T*)dout, rc2, nrc, (T*)dk, (T*)dv, S, Hq, Hkv, ldq, ldk, ldv, lddo,   \
-                     lddk, lddv, scale, sl2, skv, rt)
+                     lddk, lddv, scale, sl2, skv, rt, gk)
+    const int gk = attn_grp(g_attn_opts.dkdv_order, S / 256, Hkv * B, 1);
     if (causal) LAUNCHR(128, true); else LAUNCHR(128, false);
 #undef LAUNCHR
   } else {
@@ -1738,7 +1791,8 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
   hipLaunchKernelGGL((bwd_dkdv_kernel<T, DD, CC, NWW, ##__VA_ARGS__>), grid, dim3(NWW * 64), 0, st, (const T*)q,   \
                      (const T*)k,                                                                               \
                      (const T*)v, (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Hq, Hkv, ldq, ldk, ldv, lddo,  \
-                     lddk, lddv, scale, sl2, skv, rt)
+                     lddk, lddv, scale, sl2, skv, rt, gk)
+    const int gk = attn_grp(g_attn_opts.dkdv_order, S / (32 * nw), Hkv * B, 1);
     const bool kreg = g_attn_opts.dkdv_kreg == 1 || (g_attn_opts.dkdv_kreg < 0 && !window);
     if (nw == 8 && D == 128 && kreg) {
       if (causal) LAUNCH(128, true, 8, true); else LAUNCH(128, false, 8, true);
@@ -1808,6 +1862,12 @@ void pra_attn_set_options(int fwd_pipe, float fwd_thr, int dkdv_impl, int dq_pip
   g_attn_opts.dq_pipe = dq_pipe;
   g_attn_opts.dkdv_split = dkdv_split;
   g_attn_opts.dkdv_kreg = dkdv_kreg;
+}
+
+void pra_attn_set_order(int fwd, int dq, int dkdv) {
+  g_attn_opts.fwd_order = fwd;
+  g_attn_opts.dq_order = dq;
+  g_attn_opts.dkdv_order = dkdv;
 }
 
 long pra_attn_bwd_workspace(int dtype, int B, int S, int Hq, int Hkv, int D) {
