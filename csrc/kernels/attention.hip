@@ -56,8 +56,9 @@ namespace attn {
 // tiles of a head run together on one XCD and read its K/V tiles from HBM once, the other tiles
 // hitting that XCD's L2 (grp 0 re-reads every head's K/V from HBM once per query tile at MHA).
 // Adjacent heads (one GQA group) share an XCD.
-__device__ __forceinline__ void block_tile(int nqt, int BH, int grp, int& qt, int& bh) {
-  const int i = blockIdx.x;
+// `sched` packs the group size (bits 0-15) and the wave pairing flag (bit 16, wave_group).
+__device__ __forceinline__ void block_tile(int nqt, int BH, int sched, int& qt, int& bh) {
+  const int i = blockIdx.x, grp = sched & 0xffff;
   if (grp <= 0) {
     qt = nqt - 1 - i / BH;
     bh = i % BH;
@@ -67,6 +68,16 @@ __device__ __forceinline__ void block_tile(int nqt, int BH, int grp, int& qt, in
   const int g = j / span, r = j - g * span;
   qt = nqt - 1 - r / grp;
   bh = x * per + g * grp + r % grp;
+}
+
+// 32-row (or 32-key) group of wave `wid` in an 8-wave causal block. The waves of a workgroup are
+// placed on the SIMDs round-robin (wave w on SIMD w % 4), so by default SIMD s hosts groups s and
+// s + 4, and the SIMDs holding the long groups (most key tiles before the diagonal) finish last.
+// Paired (sched bit 16): waves 4-7 take groups 7-4, so every SIMD hosts one long and one short
+// group ((0, 7), (1, 6), (2, 5), (3, 4)) and carries the same number of tiles.
+template <int NW>
+__device__ __forceinline__ int wave_group(int wid, int sched) {
+  return NW == 8 && (sched & 0x10000) && wid >= 4 ? 11 - wid : wid;
 }
 
 
@@ -448,7 +459,7 @@ __global__ __launch_bounds__(NW * 64, PRA_FWD_MINBLK) void fwd_p_kernel(const T*
   block_tile(nqt, BH, grp, qt, bh);
   const int hq = bh % Hq, b = bh / Hq;
   const int hk = hq / (Hq / Hkv);
-  const int q0 = qt * QT, qw = q0 + wid * 32;
+  const int q0 = qt * QT, qw = q0 + wave_group<NW>(wid, grp) * 32;
 
   const T* Qb = Q + (long)b * S * ldq + hq * D;
   const T* Kb = K + (long)b * S * ldk + hk * D;
@@ -724,7 +735,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
   kbk = nkb - 1 - kbk;  // causal: early key tiles have the most work
   const int hk = bh % Hkv, b = bh / Hkv;
   const int nrep = Hq / Hkv;
-  const int k0 = kbk * KB, kw = k0 + wid * 32;
+  const int kg = wave_group<NW>(wid, grp);  // this wave's 32-key group
+  const int k0 = kbk * KB, kw = k0 + kg * 32;
   const int krow = kw + l32;
 
   {
@@ -734,8 +746,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
     gk.issue(K + ((long)b * S + k0) * ldk + hk * D, Ks);
     gv.issue(V + ((long)b * S + k0) * ldv + hk * D, Vs);
   }
-  const T* Kw = Ks + wid * 32 * D;
-  const T* Vw = Vs + wid * 32 * D;
+  const T* Kw = Ks + kg * 32 * D;
+  const T* Vw = Vs + kg * 32 * D;
   LaneOff<T, D> lo;
   lo.init(lane);
 
@@ -768,7 +780,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dkdv_kernel(
     // each wave rescales its own 32 contiguous rows (8 KiB of the image), which only it reads
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    char* kb = reinterpret_cast<char*>(Ks) + wid * 32 * D * (int)sizeof(T);
+    char* kb = reinterpret_cast<char*>(Ks) + kg * 32 * D * (int)sizeof(T);
 #pragma unroll
     for (int i = 0; i < 32 * D * (int)sizeof(T) / 1024; ++i) {
       V8<T>& c8 = *reinterpret_cast<V8<T>*>(kb + i * 1024 + lane * 16);
@@ -924,7 +936,8 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_r_kernel(
   kbk = nkb - 1 - kbk;  // causal: early key tiles have the most work
   const int hk = bh % Hkv, b = bh / Hkv;
   const int nrep = Hq / Hkv;
-  const int k0 = kbk * KB, kw = k0 + wid * 32;
+  const int kg = wave_group<NW>(wid, grp);  // this wave's 32-key group
+  const int k0 = kbk * KB, kw = k0 + kg * 32;
   const int krow = kw + l32;
 
   GStage<T, D, KB, NW> gv;
@@ -935,7 +948,7 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv_r_kernel(
   gd.init(lddo);
   const T* Kw = nullptr;
   (void)Kw;
-  const T* Vw = Vs + wid * 32 * D;
+  const T* Vw = Vs + kg * 32 * D;
   LaneOff<T, D> lo;
   lo.init(lane);
 
@@ -1304,7 +1317,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void bwd_dq_kernel(
   block_tile(nqt, BH, grp, qt, bh);
   const int hq = bh % Hq, b = bh / Hq;
   const int hk = hq / (Hq / Hkv);
-  const int q0 = qt * QT, qw = q0 + wid * 32;
+  const int q0 = qt * QT, qw = q0 + wave_group<NW>(wid, grp) * 32;
   const int qrow = qw + l32;
 
   const T* Kb = K + (long)b * S * ldk + hk * D;
@@ -1579,6 +1592,8 @@ struct AttnOptions {
   int fwd_order = 0;
   int dq_order = 0;    // the same for the dQ kernel
   int dkdv_order = 0;  // and the two-wave / ring dK/dV kernels (key tiles, lightest last)
+  // 8-wave causal blocks: pair long and short 32-row groups on each SIMD (wave_group)
+  int wave_pair = 0;
 };
 AttnOptions g_attn_opts;
 
@@ -1609,7 +1624,7 @@ hipError_t attn_fwd_t(const void* q, const void* k, const void* v, void* o, floa
   const AttnOptions& op = g_attn_opts;
   const bool pipe = (causal || skv >= S) && (op.fwd_pipe >= 0 ? op.fwd_pipe != 0 : (causal != 0));
   const float thr = op.fwd_thr;
-  const int grp = attn_grp(op.fwd_order, nqt, Hq * B, Hq / Hkv);
+  const int grp = attn_grp(op.fwd_order, nqt, Hq * B, Hq / Hkv) | (op.wave_pair ? 0x10000 : 0);
   if (op.fwd_pipe == 2 && causal && D == 128) {  // 16x16x32 forward (causal, head_dim 128)
     // (4-wave blocks, two per CU, measured 0.973 ms: the register-staged K/V tile then takes 32 VGPRs)
     hipLaunchKernelGGL((fwd16_kernel<T, NW>), grid, block, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o,
@@ -1736,7 +1751,7 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
     dim3 grid((S / (32 * nw)) * Hq * B);
     // the pipelined kernel has no key bound: padded non-causal sequences take the plain one
     const bool pipe = (causal || skv >= S) && g_attn_opts.dq_pipe != 0;
-    const int gq = attn_grp(g_attn_opts.dq_order, S / (32 * nw), Hq * B, Hq / Hkv);
+    const int gq = attn_grp(g_attn_opts.dq_order, S / (32 * nw), Hq * B, Hq / Hkv) | (g_attn_opts.wave_pair ? 0x10000 : 0);
 #define LAUNCH(DD, CC, NWW)                                                                                     \
   if (pipe)                                                                                                     \
     hipLaunchKernelGGL((bwd_dq_kernel<T, DD, CC, NWW, true>), grid, dim3(NWW * 64), 0, st, (const T*)q,       \
@@ -1782,7 +1797,7 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
   hipLaunchKernelGGL((bwd_dkdv_r_kernel<T, DD, CC>), grid, dim3(512), 0, st, (const T*)q, (const T*)k,        \
                      (const T*)v, (const T*)dout, rc2, nrc, (T*)dk, (T*)dv, S, Hq, Hkv, ldq, ldk, ldv, lddo,   \
                      lddk, lddv, scale, sl2, skv, rt, gk)
-    const int gk = attn_grp(g_attn_opts.dkdv_order, S / 256, Hkv * B, 1);
+    const int gk = attn_grp(g_attn_opts.dkdv_order, S / 256, Hkv * B, 1) | (g_attn_opts.wave_pair ? 0x10000 : 0);
     if (causal) LAUNCHR(128, true); else LAUNCHR(128, false);
 #undef LAUNCHR
   } else {
@@ -1792,7 +1807,7 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
                      (const T*)k,                                                                               \
                      (const T*)v, (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Hq, Hkv, ldq, ldk, ldv, lddo,  \
                      lddk, lddv, scale, sl2, skv, rt, gk)
-    const int gk = attn_grp(g_attn_opts.dkdv_order, S / (32 * nw), Hkv * B, 1);
+    const int gk = attn_grp(g_attn_opts.dkdv_order, S / (32 * nw), Hkv * B, 1) | (g_attn_opts.wave_pair ? 0x10000 : 0);
     const bool kreg = g_attn_opts.dkdv_kreg == 1 || (g_attn_opts.dkdv_kreg < 0 && !window);
     if (nw == 8 && D == 128 && kreg) {
       if (causal) LAUNCH(128, true, 8, true); else LAUNCH(128, false, 8, true);
@@ -1864,7 +1879,8 @@ void pra_attn_set_options(int fwd_pipe, float fwd_thr, int dkdv_impl, int dq_pip
   g_attn_opts.dkdv_kreg = dkdv_kreg;
 }
 
-void pra_attn_set_order(int fwd, int dq, int dkdv) {
+void pra_attn_set_order(int fwd, int dq, int dkdv, int wave_pair) {
+  g_attn_opts.wave_pair = wave_pair;
   g_attn_opts.fwd_order = fwd;
   g_attn_opts.dq_order = dq;
   g_attn_opts.dkdv_order = dkdv;

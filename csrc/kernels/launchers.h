@@ -95,8 +95,9 @@ hipError_t pra_attn_bwd(int dtype, const void* q, const void* k, const void* v, 
 void pra_attn_set_options(int fwd_pipe, float fwd_thr, int dkdv_impl, int dq_pipe, int dkdv_split, int dkdv_kreg,
                           int bwd_fused, int bwd_window);
 // block order of the forward / dQ / dK/dV grids: 0 = heavy tiles first, G > 0 = XCD-grouped with G heads
-// per group, -1 = by shape (attention.hip block_tile)
-void pra_attn_set_order(int fwd, int dq, int dkdv);
+// per group, -1 = by shape (attention.hip block_tile); wave_pair = 1 pairs long and short row groups
+// on each SIMD of an 8-wave block (wave_group)
+void pra_attn_set_order(int fwd, int dq, int dkdv, int wave_pair);
 // fused dQ/dK/dV backward (attention_bwd_fused.hip); ws: 2 B Hq S row constants + B Hq S 128 dQ partials
 hipError_t pra_attn_bwd_fused(int dtype, const void* q, const void* k, const void* v, const void* o, const void* dout,
                               const float* lse, float* ws, void* dq, void* dk, void* dv, int B, int S, int Hq,

@@ -70,7 +70,8 @@ def hip16(t) -> bool:
 # *_order: block order of the forward / dQ / dK/dV grids (attention.hip block_tile): -1 = XCD-grouped
 # by shape, 0 = heavy tiles first across the grid, G = XCD-grouped with G heads per group.
 _ATTN_DEFAULTS = {"fwd_pipe": -1, "fwd_thr": 8.0, "dkdv_impl": -1, "dq_pipe": -1, "dkdv_split": 1, "dkdv_kreg": -2,
-                  "bwd_fused": 0, "bwd_window": 0, "fwd_order": -1, "dq_order": -1, "dkdv_order": -1}
+                  "bwd_fused": 0, "bwd_window": 0, "fwd_order": -1, "dq_order": -1, "dkdv_order": -1,
+                  "wave_pair": 0}
 _attn_opts = dict(_ATTN_DEFAULTS)
 
 
@@ -78,7 +79,8 @@ def _attn_env() -> dict:
     env = {}
     for key, conv in (("fwd_pipe", int), ("fwd_thr", float), ("dkdv_impl", int), ("dq_pipe", int),
                       ("dkdv_split", int), ("dkdv_kreg", int), ("bwd_fused", int),
-                      ("bwd_window", int), ("fwd_order", int), ("dq_order", int), ("dkdv_order", int)):
+                      ("bwd_window", int), ("fwd_order", int), ("dq_order", int), ("dkdv_order", int),
+                      ("wave_pair", int)):
         name = "PYRECOVER_ATTN_" + key.upper()
         v = os.environ.get(name)
         if v is not None and v != "":
@@ -94,13 +96,13 @@ def _apply_options(mod, env: dict) -> None:
     opts.update(env)
     mod.attn_set_options(opts["fwd_pipe"], opts["fwd_thr"], opts["dkdv_impl"], opts["dq_pipe"], opts["dkdv_split"],
                          opts["dkdv_kreg"], opts["bwd_fused"], opts["bwd_window"])
-    mod.attn_set_order(opts["fwd_order"], opts["dq_order"], opts["dkdv_order"])
+    mod.attn_set_order(opts["fwd_order"], opts["dq_order"], opts["dkdv_order"], opts["wave_pair"])
     _attn_opts.update(opts)
 
 
 def set_attn_options(**kw) -> dict:
     """Set attention kernel selection knobs (fwd_pipe, fwd_thr, dkdv_impl, dq_pipe, dkdv_split, dkdv_kreg,
-    bwd_fused, bwd_window, fwd_order, dq_order, dkdv_order); keys left out
+    bwd_fused, bwd_window, fwd_order, dq_order, dkdv_order, wave_pair); keys left out
     keep their value, ``None`` restores the default. Returns the previous settings."""
     mod = native()  # loads the extension and applies the PYRECOVER_ATTN_* values first
     prev = dict(_attn_opts)

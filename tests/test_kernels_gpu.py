@@ -238,26 +238,27 @@ def test_attention_fwd(cuda, attn_opts, pipe, B, S, Hq, Hkv, D, causal):
                                                  (2, 768, 16, 4, 64, False)])
 @pytest.mark.parametrize("kreg", [-2, 0])
 def test_attention_block_order_is_bitwise_neutral(cuda, attn_opts, kreg, B, S, Hq, Hkv, D, causal):
-    """The XCD-grouped block order (fwd_order / dq_order / dkdv_order) only changes which workgroup
-    computes which tile: every group size gives the same bits as the heavy-first order, forward and
-    backward (ring and LDS dK/dV kernels), and matches the fp32 oracle."""
+    """The XCD-grouped block order (fwd_order / dq_order / dkdv_order) and the wave pairing only change
+    which workgroup / wave computes which tile: every setting gives the same bits as the heavy-first
+    order, forward and backward (ring and LDS dK/dV kernels), and matches the fp32 oracle."""
     C = _ext.native()
     _, q, k, v = _qkv(cuda, B, S, Hq, Hkv, D, seed=7)
     do = torch.randn(B, S, Hq, D, device=cuda).bfloat16()
     scale = 1 / math.sqrt(D)
     outs = {}
-    for order in (0, 1, 2, 4, -1):
-        attn_opts(fwd_order=order, dq_order=order, dkdv_order=order, dkdv_kreg=kreg)
+    cases = [(0, 0), (1, 0), (2, 0), (4, 0), (-1, 0), (0, 1), (-1, 1)]
+    for order, pair in cases:
+        attn_opts(fwd_order=order, dq_order=order, dkdv_order=order, dkdv_kreg=kreg, wave_pair=pair)
         o, lse = C.attn_fwd(q, k, v, scale, causal)
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         C.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, causal)
-        outs[order] = (o, lse, dq, dk, dv)
-    for order in (1, 2, 4, -1):
-        assert all(torch.equal(a, b) for a, b in zip(outs[0], outs[order])), order
+        outs[order, pair] = (o, lse, dq, dk, dv)
+    for case in cases[1:]:
+        assert all(torch.equal(a, b) for a, b in zip(outs[0, 0], outs[case])), case
     qf, kf, vf = (t.float().requires_grad_() for t in (q, k, v))
     of, _ = R.attention_lse_ref(qf, kf, vf, causal, scale)
     of.backward(do.float())
-    o, _, dq, dk, dv = outs[-1]
+    o, _, dq, dk, dv = outs[-1, 1]
     assert (o.float() - of).abs().max().item() < 2e-2
     for got, want in ((dq, qf.grad), (dk, kf.grad), (dv, vf.grad)):
         assert _rel(got, want) < 3e-2, (_rel(got, want))
