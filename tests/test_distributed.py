@@ -447,3 +447,27 @@ def test_train_bucket_cap_auto_two_ranks(tmp_path):
     argv[argv.index("--bucket-cap-mb") + 1] = "auto"
     res = _run(2, argv, tmp_path)
     assert res is not None
+
+
+def test_fp32_master_two_ranks_sharded_resume_and_reshard(tmp_path):
+    """--master-weights fp32 at W=2 with sharded checkpoints: the owners write the master next to the
+    moments, a preempted-and-resumed 2-rank run is bit-identical to an uninterrupted one (master
+    included), and the 2-rank checkpoint resumes in a single process (2 -> 1 resharding)."""
+    from pyrecover_amd.ckpt.sharded import read_sharded_state
+
+    extra = ["--distributed", "--use-torch-distributed-ckpt", "--model-dtype", "bf16", "--master-weights", "fp32"]
+    _run(2, _argv(tmp_path / "a", 4, extra), tmp_path)
+    _run(2, _argv(tmp_path / "b", 4, extra + ["--stop-at-step", "3"]), tmp_path)
+    _run(2, _argv(tmp_path / "b", 4, extra + ["--resume-from-checkpoint", "latest"]), tmp_path)
+    a = read_sharded_state(str(tmp_path / "a" / "e" / "ckpt_4"))
+    b = read_sharded_state(str(tmp_path / "b" / "e" / "ckpt_4"))
+    for k in a["model"]:
+        assert torch.equal(a["model"][k], b["model"][k]), k
+    sa, sb = a["optimizer"]["state"], b["optimizer"]["state"]
+    assert sa and all("master_param" in v for v in sa.values())
+    for i in sa:
+        for key in ("master_param", "exp_avg", "exp_avg_sq"):
+            assert sa[i][key].dtype == torch.float32 and torch.equal(sa[i][key], sb[i][key]), (i, key)
+    r = _run(1, _argv(tmp_path / "a", 6, ["--use-torch-distributed-ckpt", "--model-dtype", "bf16", "--master-weights",
+                                          "fp32", "--resume-from-checkpoint", "latest"]), tmp_path)
+    assert r["step"] == 6
