@@ -98,6 +98,9 @@ __device__ unsigned long long* pra_nt_stamp_out;
 // (Persistent workgroups walking per-XCD tile ranges through atomic counters, with the next tile's
 // prologue DMAs issued before the current tile's epilogue stores, measured 0.2-1.1% slower:
 // profiles/r4/gemm_nt_persistent_ab.log.)
+#ifndef PRA_NT_EPI2_PIPE  // SwiGLU backward epilogue with row-block loads two blocks ahead (epi2_pipe)
+#define PRA_NT_EPI2_PIPE 1
+#endif
 #ifndef PRA_NT_ST16
 #define PRA_NT_ST16 1
 #endif
@@ -220,7 +223,84 @@ __global__ __launch_bounds__(NTH) void gemm_nt_kernel(const T* __restrict__ A, c
 
   // epilogue: lane holds row m0 + 128 wm + 16 i + (l & 15), columns n0 + 128 wn + 16 j + 4 (l >> 4) + 0..3
   const int l16 = lane & 15, g4 = lane >> 4;
+
+  // SwiGLU backward epilogue (EPI 2, ST16 layout) with the g / u loads of row block i + 2 in flight
+  // while block i is computed and stored. The one-block-at-a-time form waited a full load (and the
+  // previous block's stores, which count in vmcnt) per row block: 8 serialized HBM round trips per
+  // tile, and every CU reaches its epilogue at the same time (tiles run in lockstep rounds), so the
+  // fused GEMM ran 675 us slower than the plain one at 7B W2 (profiles/r4/gemm_nt_bench_swiglu_epilogues.log),
+  // as slow as the separate kernel. The main loop's fragment registers are dead here, so the
+  // three in-flight blocks (96 VGPRs) fit.
+  auto epi2_pipe = [&](long m0, long n0) __attribute__((always_inline)) {
+    const long so = (16 * (g4 & 1) + 8 * (g4 >> 1)) - 4 * g4;
+    auto gptr = [&](int i) __attribute__((always_inline)) -> T* {
+      return C + (m0 + 128 * wm + 16 * i + l16) * ldc + n0 + 128 * wn + 4 * g4 + so;
+    };
+    uint4 gb[3][4], ub[3][4];
+    auto load = [&](int i, uint4 (&g8)[4], uint4 (&u8)[4]) __attribute__((always_inline)) {
+      const T* gp = gptr(i);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        g8[q] = *reinterpret_cast<const uint4*>(gp + 32 * q);
+        u8[q] = *reinterpret_cast<const uint4*>(gp + ep.F + 32 * q);
+      }
+    };
+    load(0, gb[0], ub[0]);
+    load(1, gb[1], ub[1]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i + 2 < 8) load(i + 2, gb[(i + 2) % 3], ub[(i + 2) % 3]);
+      const uint4 (&g8)[4] = gb[i % 3];
+      const uint4 (&u8)[4] = ub[i % 3];
+      uint2 gw[8], uw[8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {  // back to this lane's own 4 columns of blocks 2q, 2q + 1
+        const auto g0 = __builtin_amdgcn_permlane16_swap(g8[q].x, g8[q].z, false, false);
+        const auto g1 = __builtin_amdgcn_permlane16_swap(g8[q].y, g8[q].w, false, false);
+        const auto u0 = __builtin_amdgcn_permlane16_swap(u8[q].x, u8[q].z, false, false);
+        const auto u1 = __builtin_amdgcn_permlane16_swap(u8[q].y, u8[q].w, false, false);
+        gw[2 * q] = make_uint2(g0[0], g1[0]);
+        gw[2 * q + 1] = make_uint2(g0[1], g1[1]);
+        uw[2 * q] = make_uint2(u0[0], u1[0]);
+        uw[2 * q + 1] = make_uint2(u0[1], u1[1]);
+      }
+      uint2 ogw[8], ouw[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float g[4], u[4], og[4], ou[4];
+        unpack4<T>(gw[j], g);
+        unpack4<T>(uw[j], u);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {  // the math of the one-block form below, element for element
+          const float d = rnd16<T>(acc[i][j][e]);
+          const float sg = 1.f / (1.f + __expf(-g[e]));
+          const float a = rnd16<T>(g[e] * sg);
+          const float dd = rnd16<T>(d * u[e]);
+          ou[e] = d * a;
+          og[e] = dd * sg * (1.f + g[e] * (1.f - sg));
+        }
+        ogw[j] = make_uint2(pack_x2<T>(og[0], og[1]), pack_x2<T>(og[2], og[3]));
+        ouw[j] = make_uint2(pack_x2<T>(ou[0], ou[1]), pack_x2<T>(ou[2], ou[3]));
+      }
+      T* gp = gptr(i);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = 2 * q;
+        const auto g0 = __builtin_amdgcn_permlane16_swap(ogw[j].x, ogw[j + 1].x, false, false);
+        const auto g1 = __builtin_amdgcn_permlane16_swap(ogw[j].y, ogw[j + 1].y, false, false);
+        const auto u0 = __builtin_amdgcn_permlane16_swap(ouw[j].x, ouw[j + 1].x, false, false);
+        const auto u1 = __builtin_amdgcn_permlane16_swap(ouw[j].y, ouw[j + 1].y, false, false);
+        *reinterpret_cast<uint4*>(gp + 16 * j) = make_uint4(g0[0], g1[0], g0[1], g1[1]);
+        *reinterpret_cast<uint4*>(gp + ep.F + 16 * j) = make_uint4(u0[0], u1[0], u0[1], u1[1]);
+      }
+    }
+  };
+
   auto store_c = [&](long m0, long n0) __attribute__((always_inline)) {
+    if constexpr (EPI == 2 && PRA_NT_ST16 && PRA_NT_EPI2_PIPE) {
+      epi2_pipe(m0, n0);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const long row = m0 + 128 * wm + 16 * i + l16;
