@@ -1,0 +1,33 @@
+"""Documentation stays in step with the code: every PYRECOVER_* environment knob the framework reads
+(Python package, native sources, bench.py / train.py) is listed in docs/KNOBS.md."""
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PREFIXES = {"PYRECOVER_ATTN_", "PYRECOVER_RCCL_", "PYRECOVER_RCCL"}  # prefixes of documented families
+
+
+def _sources():
+    for base in ("pyrecover_amd", "csrc"):
+        for dirpath, _, files in os.walk(os.path.join(ROOT, base)):
+            for f in files:
+                if f.endswith((".py", ".h", ".cpp", ".hip")):
+                    yield os.path.join(dirpath, f)
+    for f in ("bench.py", "train.py"):
+        yield os.path.join(ROOT, f)
+
+
+def test_every_environment_knob_is_documented():
+    names = set()
+    for path in _sources():
+        with open(path, encoding="utf-8", errors="replace") as fh:
+            names.update(re.findall(r"PYRECOVER_[A-Z0-9_]+", fh.read()))
+    names -= PREFIXES
+    with open(os.path.join(ROOT, "docs", "KNOBS.md"), encoding="utf-8") as fh:
+        doc = fh.read()
+    documented = set(re.findall(r"PYRECOVER_[A-Z0-9_]+", doc))
+    # "PYRECOVER_ATTN_FWD_ORDER`, `_DQ_ORDER`" style rows document a family member by suffix
+    documented |= {"PYRECOVER_ATTN" + m for m in re.findall(r"`(_[A-Z0-9_]+)`", doc)}
+    attn_keys = {"PYRECOVER_ATTN_" + k.upper() for k in __import__("pyrecover_amd._ext", fromlist=["x"])._ATTN_DEFAULTS}
+    missing = sorted((names | attn_keys) - documented)
+    assert not missing, f"undocumented knobs (add them to docs/KNOBS.md): {missing}"
