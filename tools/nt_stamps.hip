@@ -55,12 +55,14 @@ int main(int argc, char** argv) {
   const int M = argc > 1 ? atoi(argv[1]) : 32768, N = argc > 2 ? atoi(argv[2]) : 4096;
   const int K = argc > 3 ? atoi(argv[3]) : 4096;
   const double warm = argc > 4 ? atof(argv[4]) : 2.0;
-  const int epi = argc > 5 ? atoi(argv[5]) : 0;  // 0 plain, 1 SwiGLU (C = gu [M][N], a [M][N/2])
+  const int epi = argc > 5 ? atoi(argv[5]) : 0;  // 0 plain, 1 SwiGLU (C = gu [M][N], a [M][N/2]),
+                                                   // 2 SwiGLU backward (C = gu [M][2N] read and overwritten)
   const int cus = 256;
   __bf16 *A, *B, *C;
   CK(hipMalloc(&A, (size_t)M * K * 2));
   CK(hipMalloc(&B, (size_t)N * K * 2));
-  CK(hipMalloc(&C, (size_t)M * N * 2));
+  CK(hipMalloc(&C, (size_t)M * N * 2 * (epi == 2 ? 2 : 1)));
+  if (epi == 2) hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, 0, C, 2L * M * N, 3u);
   hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, 0, A, (long)M * K, 1u);
   hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, 0, B, (long)N * K, 2u);
   const long wsf = pra_gemm_nt_ws_floats(M, N, K, cus);
@@ -87,6 +89,9 @@ int main(int argc, char** argv) {
   __bf16* C2 = nullptr;
   if (epi == 1) CK(hipMalloc(&C2, (size_t)M * (N / 2) * 2));
   auto launch = [&]() {
+    if (epi == 2)  // C is gu [M][2N], dg / du written over g / u launch after launch: timing only (the math is
+                   // checked by tests/test_gemm_nt_gpu.py)
+      return pra_gemm_nt(pra::kBF16, 2, A, B, C, M, N, K, K, K, 2L * N, nullptr, 0, N, nullptr, 0, 0, 0, ws, tk, cus, 0);
     return pra_gemm_nt(pra::kBF16, epi, A, B, C, M, N, K, K, K, N, C2, N / 2, N / 2, nullptr, 0, 0, 0, ws, tk, cus, 0);
   };
   CK(launch());
