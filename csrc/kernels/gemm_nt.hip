@@ -101,6 +101,9 @@ __device__ unsigned long long* pra_nt_stamp_out;
 #ifndef PRA_NT_EPI2_PIPE  // SwiGLU backward epilogue with row-block loads two blocks ahead (epi2_pipe)
 #define PRA_NT_EPI2_PIPE 1
 #endif
+#ifndef PRA_NT_EPI2_DEPTH  // row blocks of g / u in flight in epi2_pipe (32 VGPRs each)
+#define PRA_NT_EPI2_DEPTH 3
+#endif
 #ifndef PRA_NT_ST16
 #define PRA_NT_ST16 1
 #endif
@@ -236,7 +239,8 @@ __global__ __launch_bounds__(NTH) void gemm_nt_kernel(const T* __restrict__ A, c
     auto gptr = [&](int i) __attribute__((always_inline)) -> T* {
       return C + (m0 + 128 * wm + 16 * i + l16) * ldc + n0 + 128 * wn + 4 * g4 + so;
     };
-    uint4 gb[3][4], ub[3][4];
+    constexpr int DEPTH = PRA_NT_EPI2_DEPTH;  // row blocks in flight
+    uint4 gb[DEPTH][4], ub[DEPTH][4];
     auto load = [&](int i, uint4 (&g8)[4], uint4 (&u8)[4]) __attribute__((always_inline)) {
       const T* gp = gptr(i);
 #pragma unroll
@@ -245,13 +249,13 @@ __global__ __launch_bounds__(NTH) void gemm_nt_kernel(const T* __restrict__ A, c
         u8[q] = *reinterpret_cast<const uint4*>(gp + ep.F + 32 * q);
       }
     };
-    load(0, gb[0], ub[0]);
-    load(1, gb[1], ub[1]);
+#pragma unroll
+    for (int i = 0; i < DEPTH - 1; ++i) load(i, gb[i], ub[i]);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      if (i + 2 < 8) load(i + 2, gb[(i + 2) % 3], ub[(i + 2) % 3]);
-      const uint4 (&g8)[4] = gb[i % 3];
-      const uint4 (&u8)[4] = ub[i % 3];
+      if (i + DEPTH - 1 < 8) load(i + DEPTH - 1, gb[(i + DEPTH - 1) % DEPTH], ub[(i + DEPTH - 1) % DEPTH]);
+      const uint4 (&g8)[4] = gb[i % DEPTH];
+      const uint4 (&u8)[4] = ub[i % DEPTH];
       uint2 gw[8], uw[8];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {  // back to this lane's own 4 columns of blocks 2q, 2q + 1
