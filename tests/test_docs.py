@@ -1,5 +1,5 @@
-"""Documentation stays in step with the code: every PYRECOVER_* environment knob the framework reads
-(Python package, native sources, bench.py / train.py) is listed in docs/KNOBS.md."""
+"""Documentation stays in step with the code: every PYRECOVER_* / PRA_* environment knob the framework
+reads (Python package, native sources, bench.py / train.py) is listed in docs/KNOBS.md."""
 import os
 import re
 
@@ -21,11 +21,14 @@ def test_every_environment_knob_is_documented():
     names = set()
     for path in _sources():
         with open(path, encoding="utf-8", errors="replace") as fh:
-            names.update(re.findall(r"PYRECOVER_[A-Z0-9_]+", fh.read()))
+            text = fh.read()
+        names.update(re.findall(r"PYRECOVER_[A-Z0-9_]+", text))
+        # PRA_* names are also compile-time macros; only the ones read from the environment count
+        names.update(re.findall(r"(?:environ\.get|getenv)\(\s*[\"'](PRA_[A-Z0-9_]+)", text))
     names -= PREFIXES
     with open(os.path.join(ROOT, "docs", "KNOBS.md"), encoding="utf-8") as fh:
         doc = fh.read()
-    documented = set(re.findall(r"PYRECOVER_[A-Z0-9_]+", doc))
+    documented = set(re.findall(r"(?:PYRECOVER|PRA)_[A-Z0-9_]+", doc))
     # "PYRECOVER_ATTN_FWD_ORDER`, `_DQ_ORDER`" style rows document a family member by suffix
     documented |= {"PYRECOVER_ATTN" + m for m in re.findall(r"`(_[A-Z0-9_]+)`", doc)}
     attn_keys = {"PYRECOVER_ATTN_" + k.upper() for k in __import__("pyrecover_amd._ext", fromlist=["x"])._ATTN_DEFAULTS}
