@@ -1584,9 +1584,12 @@ struct AttnOptions {
   // dK/dV kernel hosts (with the update 1045.4 vs 1048.3 ms; profiles/r5/attn_fused/). The choice must
   // not depend on the window (dQ differs in the last bits), so it is a run-wide setting.
   int bwd_fused = 0;
-  // where the side-stream window (mid_event) opens in the split backward: 0 = between the dQ and the
-  // dK/dV kernels (default), 1 = before the dQ kernel (the update then runs beside both)
-  int bwd_window = 0;
+  // where the side-stream window (mid_event) opens in the split backward: 0 = between the dQ and
+  // the dK/dV kernels, 1 = before the dQ kernel (the update then runs beside both), -1 (default) = by
+  // shape (window_before_dq): before dQ at <= 4096 tokens per call, where the dK/dV kernel alone is
+  // too short a window (same-process A/B: Llama-3-8B B1 S2048 110.06 -> 109.61 ms, 7B B1 98.62 ->
+  // 97.96 ms; 7B B16 0.5% slower; profiles/r5/adamw/). Bitwise neutral: only the event moves.
+  int bwd_window = -1;
   // block order of the pipelined forward (block_tile): 0 = heavy query tiles first across the grid,
   // G > 0 = XCD-grouped, G heads per group; -1 = by shape (attn_grp)
   int fwd_order = 0;
@@ -1596,6 +1599,11 @@ struct AttnOptions {
   int wave_pair = 0;
 };
 AttnOptions g_attn_opts;
+
+static bool window_before_dq(int B, int S) {
+  const int w = g_attn_opts.bwd_window;
+  return w == 1 || (w < 0 && (long)B * S <= 4096);
+}
 
 // Heads per XCD group for an nqt x BH grid under option `order`, 0 when the grid does not split.
 // By shape (order < 0): at least the rep = Hq / Hkv query heads that share a kv head (forward and dQ
@@ -1743,7 +1751,8 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
                     nw == 8 && D == 128;  // bwd_dkdv_r_kernel
   float* rc2 = (p2 || ring) ? delta + nrc : nullptr;
   // dQ first: it also computes delta = rowsum(dO * O), which the dK/dV kernel reads
-  if (mid_event != nullptr && g_attn_opts.bwd_window == 1) {
+  const bool win_early = window_before_dq(B, S);
+  if (mid_event != nullptr && win_early) {
     const hipError_t e = hipEventRecord(mid_event, st);
     if (e != hipSuccess) return e;
   }
@@ -1770,7 +1779,7 @@ hipError_t attn_bwd_t(const void* q, const void* k, const void* v, const void* o
     }
 #undef LAUNCH
   }
-  if (mid_event != nullptr && g_attn_opts.bwd_window != 1) {  // between dQ and dK/dV
+  if (mid_event != nullptr && !win_early) {  // between dQ and dK/dV
     const hipError_t e = hipEventRecord(mid_event, st);
     if (e != hipSuccess) return e;
   }

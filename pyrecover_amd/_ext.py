@@ -70,7 +70,7 @@ def hip16(t) -> bool:
 # *_order: block order of the forward / dQ / dK/dV grids (attention.hip block_tile): -1 = XCD-grouped
 # by shape, 0 = heavy tiles first across the grid, G = XCD-grouped with G heads per group.
 _ATTN_DEFAULTS = {"fwd_pipe": -1, "fwd_thr": 8.0, "dkdv_impl": -1, "dq_pipe": -1, "dkdv_split": 1, "dkdv_kreg": -2,
-                  "bwd_fused": 0, "bwd_window": 0, "fwd_order": -1, "dq_order": -1, "dkdv_order": -1,
+                  "bwd_fused": 0, "bwd_window": -1, "fwd_order": -1, "dq_order": -1, "dkdv_order": -1,
                   "wave_pair": 0}
 _attn_opts = dict(_ATTN_DEFAULTS)
 
