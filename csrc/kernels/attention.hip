@@ -1588,7 +1588,8 @@ struct AttnOptions {
   // the dK/dV kernels, 1 = before the dQ kernel (the update then runs beside both), -1 (default) = by
   // shape (window_before_dq): before dQ at <= 4096 tokens per call, where the dK/dV kernel alone is
   // too short a window (same-process A/B: Llama-3-8B B1 S2048 110.06 -> 109.61 ms, 7B B1 98.62 ->
-  // 97.96 ms; 7B B16 0.5% slower; profiles/r5/adamw/). Bitwise neutral: only the event moves.
+  // 97.96 ms; at 8192 tokens slower: 8B S8192 B1 +2.35%, 8B S2048 B4 +0.33%, 7B B16 +0.5%;
+  // profiles/r5/window/). Bitwise neutral: only the event moves.
   int bwd_window = -1;
   // block order of the pipelined forward (block_tile): 0 = heavy query tiles first across the grid,
   // G > 0 = XCD-grouped, G heads per group; -1 = by shape (attn_grp)
