@@ -100,11 +100,17 @@ def _adamw_fast() -> bool:
     return adamw.FAST_MATH
 
 
-def _opt_sched() -> str:
+def _opt_sched(tokens: int = 0) -> str:
+    """Where the overlapped AdamW update runs; `tokens` = B * S of one attention call (the window
+    opens before the dQ kernel at <= 4096 tokens unless PYRECOVER_ATTN_BWD_WINDOW pins it)."""
+    from pyrecover_amd import _ext
     from pyrecover_amd.optim import adamw
 
-    return {"attn": "beside the attention dK/dV kernels", "eager": "per bucket as reduced"}.get(
-        adamw.OPT_SCHED, adamw.OPT_SCHED)
+    if adamw.OPT_SCHED == "attn":
+        w = _ext._attn_opts.get("bwd_window", -1)
+        early = w == 1 or (w < 0 and 0 < tokens <= 4096)
+        return "beside the attention dQ and dK/dV kernels" if early else "beside the attention dK/dV kernels"
+    return {"eager": "per bucket as reduced"}.get(adamw.OPT_SCHED, adamw.OPT_SCHED)
 
 
 def main():
@@ -285,7 +291,7 @@ def main():
                        "grad_buckets": reducer.num_buckets,
                        "rccl_high_priority_stream": os.environ.get("PYRECOVER_RCCL_HIGH_PRIORITY", "1") == "1",
                        "optimizer": "AdamW (flat fused HIP)" + ("" if args.no_overlap_optimizer else
-                                                                 f", overlapped with backward ({_opt_sched()})"),
+                                                                 f", overlapped with backward ({_opt_sched(B * S)})"),
                        "adamw_math": "hw rcp/sqrt (fast)" if _adamw_fast() else "torch _fused_adamw_ bit-exact",
                        "weight_shadows": bool(getattr(flat, "t_mats", None)),
                        "hand_written_gemms": _gemm_sites(B * S, cfg.dim)},
