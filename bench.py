@@ -59,6 +59,10 @@ def parse():
                     help="record device events around forward / backward / optimizer of each timed step")
     ap.add_argument("--no-comm-timing", action="store_true",
                     help="W > 1: skip the per-bucket collective timing (events; no host sync in the step)")
+    ap.add_argument("--shard-optimizer", action="store_true",
+                    help="W > 1: ZeRO-1 (reduce-scatter, 1/W AdamW update, parameter all-gather; train.py flag)")
+    ap.add_argument("--sparse-embedding-grad", choices=["auto", "on", "off"], default="auto",
+                    help="W > 1: token-embedding gradient as (id, row) pairs (auto: tokens per step <= vocab / 2)")
     ap.add_argument("--cpu", action="store_true",
                     help="run on the CPU over gloo (tests of the launcher and the DDP path; not a benchmark)")
     ap.add_argument("--gemm-tuning", choices=["auto", "off", "tune"], default="auto",
@@ -164,15 +168,20 @@ def main():
         torch.set_default_dtype(torch.bfloat16)
         model = Transformer(cfg)
         torch.set_default_dtype(prev)
-    flat = model.flatten_(tokens_per_step=args.batch_per_gpu * args.seq_len)
+    shard = args.shard_optimizer and world > 1
+    flat = model.flatten_(tokens_per_step=args.batch_per_gpu * args.seq_len, shadows=False if shard else None)
     if world > 1:
         broadcast_flat(flat)
     bucket_tune = None
     if args.bucket_mb == "auto":
         from pyrecover_amd.parallel.bucket_tune import autotune_bucket_mb
 
-        args.bucket_mb, bucket_tune = autotune_bucket_mb(dev, flat.grad.dtype)
-    reducer = GradReducer(flat, bucket_cap_mb=args.bucket_mb, backend=args.allreduce)
+        args.bucket_mb, bucket_tune = autotune_bucket_mb(dev, flat.grad.dtype, backend=args.allreduce)
+    from pyrecover_amd.trainer import _use_sparse_embedding
+
+    sparse = _use_sparse_embedding(args.sparse_embedding_grad, world, args.batch_per_gpu * args.seq_len, cfg.vocab_size)
+    reducer = GradReducer(flat, bucket_cap_mb=args.bucket_mb, backend=args.allreduce, shard=shard,
+                          sparse_slot=flat.slot(model.tok_embeddings.weight).index if sparse else None)
     timer = reducer.enable_comm_timing() if world > 1 and not args.no_comm_timing else None
     opt = FlatAdamW(flat, lr=args.lr, fused=True, grad_scale=1.0 / world,
                     master_weights=args.master_weights == "fp32")
@@ -252,6 +261,10 @@ def main():
         torch.distributed.all_reduce(dt_t, op=torch.distributed.ReduceOp.MAX)
     dt = float(dt_t.item())
     final_loss = float(loss.item())
+    # after the clock stopped: are the replicas still identical? (parallel/consistency.py)
+    from pyrecover_amd.parallel.consistency import replica_report
+
+    replicas = replica_report(flat, opt)
     tokens = B * S * world * args.steps
     tps = tokens / dt
     n_params = model.num_params()
@@ -284,6 +297,8 @@ def main():
                        "bucket_mb": args.bucket_mb if world > 1 else None,
                        "bucket_autotune": bucket_tune,
                        "master_weights": args.master_weights,
+                       "shard_optimizer": shard,
+                       "sparse_embedding_grad": bool(sparse and world > 1),
                        "allreduce": (None if world == 1 else "xgmi" if args.allreduce == "xgmi" else
                                      "rccl" if torch.distributed.get_backend() == "nccl" else
                                      torch.distributed.get_backend()),
@@ -302,7 +317,11 @@ def main():
             "peak_mem_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if dev.type == "cuda" else None,
             "gemm_table": bool(torch.cuda.tunable.is_enabled()) if dev.type == "cuda" else False,
             "hip_graph": bool(args.graph),
+            "params_identical_across_ranks": replicas["params_identical_across_ranks"],
+            "optimizer_identical_across_ranks": replicas["optimizer_identical_across_ranks"],
         }
+        if replicas["mismatched"]:
+            out["replica_checksums"] = {k: replicas["checksums"][k] for k in replicas["mismatched"]}
         if world > 1:
             out["comm"] = comm
             out["comm_env"] = comm_env()
@@ -317,6 +336,9 @@ def main():
         flush_tuning()
     if world > 1:
         torch.distributed.destroy_process_group()
+    if replicas["mismatched"]:
+        print(f"error: replicas differ across ranks after the timed steps: {replicas['mismatched']}", file=sys.stderr)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -91,7 +91,7 @@ def main():
     shutil.rmtree(args.dir, ignore_errors=True)
     os.makedirs(args.dir, exist_ok=True)
     out = {"metric": "checkpoint save+resume wall-clock", "model": f"{args.model}-shape",
-           "params": model.num_params(), "state_bytes": 3 * flat.state_bytes(), "step_s": round(step_s, 3),
+           "params": model.num_params(), "state_bytes": opt.checkpoint_bytes(), "step_s": round(step_s, 3),
            "dir": args.dir, "whole_file_md5": os.environ.get("PYRECOVER_WHOLE_MD5", "1") != "0"}
     ref_params = flat.data.clone()
     ref_v = opt.exp_avg_sq.clone()
@@ -136,7 +136,7 @@ def main():
         p = os.path.join(args.dir, "ckpt_3.pt")
         # as train.py --async-checkpoint does: the pinned pool is allocated before training runs,
         # so the first save does not pay for it
-        core.Checkpointer.get(flat.data.device).prewarm(int(3 * flat.state_bytes() * 1.05) + (64 << 20),
+        core.Checkpointer.get(flat.data.device).prewarm(int(opt.checkpoint_bytes() * 1.05) + (64 << 20),
                                                         background=False)
         step()
         step()

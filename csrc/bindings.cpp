@@ -648,6 +648,22 @@ at::Tensor grad_norm(const at::Tensor& x, double max_norm, double pre_scale) {
   return out;
 }
 
+// replica checksum of a contiguous buffer: {fp64 sum of its elements, 64-bit word hash (int64 bits)}
+std::vector<at::Tensor> checksum(const at::Tensor& x) {
+  const Range range_("pyrecover::checksum");
+  check_dev(x, "x");
+  TORCH_CHECK(x.is_contiguous(), "checksum: contiguous");
+  const c10::DeviceGuard guard(x.device());
+  const int nb = pra_checksum_blocks();
+  auto sum = at::empty({1}, x.options().dtype(at::kDouble)), hash = at::empty({1}, x.options().dtype(at::kLong));
+  auto ws_s = at::empty({nb}, x.options().dtype(at::kDouble)), ws_h = at::empty({nb}, x.options().dtype(at::kLong));
+  check(pra_checksum(dt(x), x.data_ptr(), x.numel() * x.element_size(), ws_s.data_ptr<double>(),
+                     reinterpret_cast<unsigned long long*>(ws_h.data_ptr<int64_t>()), sum.data_ptr<double>(),
+                     reinterpret_cast<unsigned long long*>(hash.data_ptr<int64_t>()), stream_of(x)),
+        "checksum");
+  return {sum, hash};
+}
+
 // q/k/v/o views [B, S, H, D] with stride(3)==1, stride(2)==D, stride(0)==S*stride(1).
 void check_bshd(const at::Tensor& t, const char* name, int64_t B, int64_t S, int64_t H, int64_t D,
                 at::ScalarType dtype) {
@@ -814,6 +830,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("gscale"), py::arg("gscale_dev") = py::none(), py::arg("hyper_dev") = py::none(),
         py::arg("fast") = false);
   m.def("grad_norm", &grad_norm);
+  m.def("checksum", &checksum);
   m.def("wgrad_mm_", &wgrad_mm_);
   m.def("wgrad_mm_exp_", &wgrad_mm_exp_);
   m.def("wgrad_set_streamk", &pra_wgrad_set_streamk,

@@ -145,3 +145,75 @@ extern "C" hipError_t pra_pull_gather(const void* const* srcs, void* const* dsts
   hipLaunchKernelGGL(pra::pull_gather_kernel, dim3((unsigned)bx, (unsigned)n), dim3(256), 0, s, l);
   return hipGetLastError();
 }
+
+// Replica checksum (pyrecover_amd/parallel/consistency.py): a 64-bit position-weighted hash of a
+// buffer's 32-bit words, h = sum_i w_i (2 i + 1) mod 2^64, and the fp64 sum of its elements. Two
+// replicas of a parameter / moment buffer agree on both only if they are (almost surely) bitwise
+// equal; the hash changes when any word changes or two words swap. Two passes (per-block partials,
+// then one ordered sum): integer results are exact in any order and the fp64 sum is reproducible
+// on identical data, with no atomics.
+namespace pra {
+template <typename T>
+__global__ __launch_bounds__(256) void checksum_kernel(const uint4* __restrict__ x, long n16, double* __restrict__ psum,
+                                                       unsigned long long* __restrict__ phash) {
+  constexpr int E = 16 / sizeof(T);  // elements per 16-B vector
+  double s = 0.0;
+  unsigned long long h = 0ull;
+  const long stride = (long)gridDim.x * 256;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride) {
+    const uint4 v = x[i];
+    const unsigned long long w0 = 4ull * (unsigned long long)i;
+    h += (unsigned long long)v.x * (2ull * w0 + 1ull) + (unsigned long long)v.y * (2ull * w0 + 3ull) +
+         (unsigned long long)v.z * (2ull * w0 + 5ull) + (unsigned long long)v.w * (2ull * w0 + 7ull);
+    const T* e = reinterpret_cast<const T*>(&v);
+    float part = 0.f;
+#pragma unroll
+    for (int j = 0; j < E; ++j) part += to_f<T>(e[j]);
+    s += (double)part;
+  }
+  __shared__ double ss[256];
+  __shared__ unsigned long long hh[256];
+  ss[threadIdx.x] = s;
+  hh[threadIdx.x] = h;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      ss[threadIdx.x] += ss[threadIdx.x + o];
+      hh[threadIdx.x] += hh[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    psum[blockIdx.x] = ss[0];
+    phash[blockIdx.x] = hh[0];
+  }
+}
+__global__ __launch_bounds__(64) void checksum_final_kernel(const double* __restrict__ psum,
+                                                            const unsigned long long* __restrict__ phash, int nb,
+                                                            double* __restrict__ out_sum,
+                                                            unsigned long long* __restrict__ out_hash) {
+  if (threadIdx.x != 0) return;
+  double s = 0.0;
+  unsigned long long h = 0ull;
+  for (int i = 0; i < nb; ++i) {
+    s += psum[i];
+    h += phash[i];
+  }
+  out_sum[0] = s;
+  out_hash[0] = h;
+}
+}  // namespace pra
+
+extern "C" int pra_checksum_blocks() { return 1024; }
+
+// ws: pra_checksum_blocks() doubles + as many u64; nbytes % 16 == 0, 16-B aligned
+extern "C" hipError_t pra_checksum(int dtype, const void* x, long nbytes, double* ws_sum, unsigned long long* ws_hash,
+                                   double* out_sum, unsigned long long* out_hash, hipStream_t s) {
+  if (nbytes % 16 || reinterpret_cast<uintptr_t>(x) % 16) return hipErrorInvalidValue;
+  const int nb = pra_checksum_blocks();
+  PRA_DISPATCH_FLOAT(dtype, T,
+                     hipLaunchKernelGGL((pra::checksum_kernel<T>), dim3(nb), dim3(256), 0, s, (const uint4*)x,
+                                        nbytes / 16, ws_sum, ws_hash));
+  hipLaunchKernelGGL(pra::checksum_final_kernel, dim3(1), dim3(64), 0, s, ws_sum, ws_hash, nb, out_sum, out_hash);
+  return hipGetLastError();
+}

@@ -75,6 +75,9 @@ hipError_t pra_grad_norm(int dtype, const void* x, long n, float* ws, float* out
 
 // dst <- src, nbytes, device memory (16-B vector path when both are 16-B aligned)
 hipError_t pra_copy_d2d(void* dst, const void* src, long nbytes, hipStream_t s);
+int pra_checksum_blocks();
+hipError_t pra_checksum(int dtype, const void* x, long nbytes, double* ws_sum, unsigned long long* ws_hash,
+                        double* out_sum, unsigned long long* out_hash, hipStream_t s);
 hipError_t pra_sum_slices(int dtype, const void* const* srcs, int nsrc, void* dst, long n, hipStream_t s);
 // n (<= 16) copies src[k] -> dst[k] of nbytes[k] in one kernel (16-B aligned pointers)
 hipError_t pra_pull_gather(const void* const* srcs, void* const* dsts, const long* nbytes, int n, hipStream_t s);

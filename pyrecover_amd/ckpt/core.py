@@ -129,6 +129,38 @@ def warn_reduction_change(ps: Optional[Dict[str, Any]]) -> List[str]:
     return diffs
 
 
+def peek_reduction(path: str, exp_dir: Optional[Path] = None, distributed: bool = False) -> Optional[Dict[str, Any]]:
+    """The gradient-reduction settings a checkpoint was written with (``pyrecover_state.reduction``),
+    read without loading its tensors (``latest`` resolves as the loaders do); None if there is none."""
+    try:
+        if path == "latest":
+            path = get_latest_checkpoint(str(exp_dir), distributed) if exp_dir is not None else None
+            if path is None:
+                return None
+        p = Path(path)
+        if p.is_dir():
+            from .sharded import read_metadata, read_sharded_state
+
+            keep = [i.fqn for i in read_metadata(p).storage_data if i.fqn.startswith("pyrecover_state.reduction")]
+            skip = {i.fqn for i in read_metadata(p).storage_data} - set(keep)
+            st = read_sharded_state(str(p), skip=skip)
+        else:
+            # mmap: the tensors' bytes are not read
+            st = torch.load(str(p), map_location="cpu", mmap=True, weights_only=True)
+        return ((st or {}).get("pyrecover_state") or {}).get("reduction")
+    except Exception as e:  # noqa: BLE001 - an unreadable checkpoint fails later, in the loader
+        logger.warning(f"could not read the reduction settings of {path}: {e}")
+        return None
+
+
+def prepare_optimizer_state(optimizer):
+    """Collective, on every rank before a save: the sharded optimizer all-gathers its moments so the
+    checkpoint holds the full state (a no-op for the replicated optimizer)."""
+    fn = getattr(optimizer, "gather_state", None)
+    if fn is not None:
+        fn()
+
+
 def build_state(model, optimizer, lr_scheduler=None, sampler=None, step: int = 0, epoch: Optional[int] = None,
                 extra: Optional[Dict[str, Any]] = None,
                 rng_per_rank: Optional[List[Dict[str, Any]]] = None) -> Dict[str, Any]:
@@ -485,14 +517,23 @@ class SaveCostModel:
         return max(write_rem + final_budget, digest_end) - final_budget
 
 
-def drop_unverified(base: Path, keep: str) -> List[str]:
+# vanilla checkpoints whose whole-file .md5 this process left to a deferred background digest
+DEFERRED_MD5_PATHS: set = set()
+
+
+def drop_unverified(base: Path, keep: str, only: Optional[set] = None) -> List[str]:
     """After a time-aware stop whose final checkpoint carries its ``.md5``: remove older vanilla
-    checkpoints that have no ``.md5`` (a deferred digest cut short at the wall-clock limit), so
-    with ``--verify-checkpoints`` every checkpoint left on disk verifies with the reference's
-    loader (reference pyrecover/checkpoint.py:157-175). Returns the removed paths."""
+    checkpoints whose deferred digest THIS process queued and abandoned at the wall-clock limit (no
+    ``.md5``), so with ``--verify-checkpoints`` every checkpoint this job wrote verifies with the
+    reference's loader (reference pyrecover/checkpoint.py:157-175). Checkpoints of earlier jobs
+    (e.g. written without --verify-checkpoints) are never touched. ``only`` defaults to
+    :data:`DEFERRED_MD5_PATHS`. Returns the removed paths."""
     removed = []
+    only = DEFERRED_MD5_PATHS if only is None else only
     keep_step = ckpt_step(Path(keep))
     for f in Path(base).glob("ckpt_*.pt"):
+        if str(f) not in only:
+            continue
         if str(f) == str(keep) or ckpt_step(f) >= keep_step or Path(str(f) + ".md5").exists():
             continue
         try:

@@ -99,6 +99,7 @@ def save_ckpt_distributed(model, optimizer, lr_scheduler=None, sampler=None, ste
         dist.barrier()
     core.wait_all()
     finalize_pending()
+    core.prepare_optimizer_state(optimizer)  # collective: a sharded optimizer gathers its moments
     rngs = core.gather_rng_states() if is_distributed else None  # collective: every rank's streams
     state = core.build_state(model, optimizer, lr_scheduler, sampler, step, epoch, extra_state, rngs)
     # dcp key layout: "metadata" holds epoch/step (reference checkpoint.py:254-258)

@@ -46,6 +46,7 @@ def save_ckpt_vanilla(model, optimizer, lr_scheduler=None, sampler=None, step: i
     inline, so the sidecar exists when the save returns (the time-aware final checkpoint)."""
     if is_distributed:
         dist.barrier()
+    core.prepare_optimizer_state(optimizer)  # collective: a sharded optimizer gathers its moments
     rngs = core.gather_rng_states() if is_distributed else None  # collective: every rank's streams
     if rank == 0 or not is_distributed:
         state = core.build_state(model, optimizer, lr_scheduler, sampler, step, epoch, extra_state, rngs)
@@ -69,6 +70,8 @@ def save_ckpt_vanilla(model, optimizer, lr_scheduler=None, sampler=None, step: i
         if defer_md5 is None:
             defer_md5 = os.environ.get("PYRECOVER_DEFER_MD5", "1") != "0"
         defer = verify and defer_md5
+        if defer:
+            core.DEFERRED_MD5_PATHS.add(str(checkpoint_path))
         ck.write(str(checkpoint_path), [("zip", records)], verify, fsync, (staged, keep), done, defer_md5=defer)
         if not async_save:
             ck.wait()

@@ -101,6 +101,15 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--allreduce", choices=["rccl", "xgmi"], default="rccl",
                    help="gradient all-reduce backend: RCCL rings (default) or the direct per-link xGMI "
                         "reduce-scatter/all-gather over IPC-mapped peer buffers (single node)")
+    p.add_argument("--shard-optimizer", action="store_true",
+                   help="ZeRO-1 data parallelism: reduce-scatter each gradient bucket, update only this rank's "
+                        "1/W of the parameters, all-gather them (replicated parameters, unchanged checkpoints)")
+    p.add_argument("--sparse-embedding-grad", choices=["auto", "on", "off"], default="auto",
+                   help="reduce the token-embedding gradient as (token id, row) pairs instead of a dense "
+                        "all-reduce; auto: when the ranks' tokens per step are at most half the vocabulary")
+    p.add_argument("--replica-check-every", type=int, default=None,
+                   help="W > 1: compare a checksum of the parameters (and optimizer moments) across ranks every "
+                        "N steps and at the end, and stop on a mismatch (default 10 x --logging-frequency; 0 = off)")
     p.add_argument("--async-checkpoint", action="store_true",
                    help="snapshot to pinned host memory and write in the background while training continues")
     p.add_argument("--no-fsync", action="store_true", help="skip fsync of checkpoint files")

@@ -197,19 +197,21 @@ class Transformer(nn.Module):
         g.append([("output.weight", self.output.weight)])
         return g
 
-    def flatten_(self, tokens_per_step: Optional[int] = None) -> FlatParams:
+    def flatten_(self, tokens_per_step: Optional[int] = None, shadows: Optional[bool] = None) -> FlatParams:
         """Move all parameters/gradients into flat buffers (call after the final .to(device/dtype)).
 
         Transposed weight shadows (K-contiguous W^T for the data-gradient GEMMs, rewritten by the
         optimizer): +3.5% at 7B B16 (profiles/ab_weight_shadows_s7.log), +5% at 7B B1 (99.1 vs
         104.1-104.4 ms), -0.5% at Llama-3-8B B1 (108.1 vs 107.6 ms; profiles/r4/shadow_policy_b1/),
-        so they are on at every batch size. PRA_WEIGHT_SHADOWS=0 turns them off;
-        PRA_WEIGHT_SHADOWS_HEAD=0 leaves the output head without one."""
+        so they are on at every batch size. PRA_WEIGHT_SHADOWS=0 (or ``shadows=False``: the sharded
+        optimizer, whose owned chunks cut matrices, would re-derive every shadow after the parameter
+        all-gather) turns them off; PRA_WEIGHT_SHADOWS_HEAD=0 leaves the output head without one."""
         if self.flat is None:
             self.flat = FlatParams(self.fusion_groups())
             # optimizer-state indices follow model.parameters() order, as in the reference
             self.flat.module_order = list(self.parameters())
-            shadows = os.environ.get("PRA_WEIGHT_SHADOWS", "1") != "0"
+            if shadows is None:
+                shadows = os.environ.get("PRA_WEIGHT_SHADOWS", "1") != "0"
             head = os.environ.get("PRA_WEIGHT_SHADOWS_HEAD", "1") == "1"
             for mats in self._gemm_weights(head) if shadows else []:
                 self.flat.register_transposed(mats, (sum(p.shape[0] for p in mats), mats[0].shape[1]))

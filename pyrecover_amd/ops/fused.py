@@ -311,6 +311,10 @@ class _Embedding(torch.autograd.Function):
         slot = ctx.slot
         buf, acc = slot.begin(dout)
         V, D = ctx.shape
+        gs = getattr(slot, "s", None)
+        if gs is not None:  # the rows this gradient touches, for a sparse exchange (parallel/ddp.py)
+            prev = gs.sparse_ids if acc else None
+            gs.sparse_ids = ids.reshape(-1) if prev is None else torch.cat([prev, ids.reshape(-1)])
         if _vec_hip(dout, D):
             _ext.require_for(dout).embedding_bwd(ids.contiguous(), dout.contiguous(), buf.view(V, D), acc)
         else:

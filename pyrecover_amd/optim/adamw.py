@@ -70,6 +70,7 @@ class FlatAdamW(torch.optim.AdamW):
         if len(self.param_groups) != 1:
             raise ValueError("FlatAdamW supports a single param group (the reference uses one)")
         self.flat = flat
+        flat.layout_frozen = True  # the moments below are laid out like the flat buffers
         self.grad_scale = grad_scale  # e.g. 1/world_size after a SUM all-reduce
         self.grad_scale_dev: Optional[torch.Tensor] = None  # device-side multiplier (clipping)
         # fp32 master + fp32 moments for 16-bit parameters (fp32 / fp64 models already update in place)
@@ -84,7 +85,8 @@ class FlatAdamW(torch.optim.AdamW):
         self.overlap = False
         self._in_step = False
         self._done_ranges = []
-        self._held = []  # (lo, hi, work) of reduced buckets not yet enqueued (OPT_SCHED "attn")
+        self._held = []  # (bucket, lo, hi, work) of reduced buckets not yet enqueued (OPT_SCHED "attn")
+        self._gathers = []  # parameter all-gathers issued behind the updates (sharded optimizer)
         self._window_seen = False  # an attention window released held buckets (HIP attention path)
         self.pre_update_fences = []  # callables run on the update stream before any update
         # graph mode (train.py --compile): step-dependent scalars come from device memory
@@ -145,11 +147,18 @@ class FlatAdamW(torch.optim.AdamW):
         m, v = self.exp_avg, self.exp_avg_sq
 
         fast = FAST_MATH
+        sharded = self._sharded()
         if self.master is not None:
             # fp32 master update, then the transposed shadows of the matrices in range from the
-            # rounded parameters (same stream: the next backward sees them)
+            # rounded parameters (same stream: the next backward sees them; sharded: after the gather)
             C.adamw_master_(f.data[lo:hi], self.master[lo:hi], f.grad[lo:hi], m[lo:hi], v[lo:hi], *args, fast)
-            f.refresh_transposed(lo, hi)
+            if not sharded:
+                f.refresh_transposed(lo, hi)
+            return
+        if sharded:
+            # an owned chunk cuts matrices: plain update; the shadows are re-derived from the gathered
+            # parameters (step)
+            C.adamw_flat_(f.data[lo:hi], f.grad[lo:hi], m[lo:hi], v[lo:hi], *args, fast)
             return
 
         def flat_update(a, b):
@@ -185,14 +194,13 @@ class FlatAdamW(torch.optim.AdamW):
         if self.stream is None:
             if work is not None:
                 work.wait()
-            self._update_range(lo, hi)
-            self._done_ranges.append((lo, hi))
+            self._update_bucket(b, lo, hi)
             return
         if self._held and not self._window_seen:
             # no attention window has released held buckets yet: this model's backward may offer
             # none, so do not wait any longer than one bucket
             self.release_held()
-        self._held.append((lo, hi, work))
+        self._held.append((b, lo, hi, work))
         if OPT_SCHED != "attn":
             self.release_held()
 
@@ -209,14 +217,54 @@ class FlatAdamW(torch.optim.AdamW):
             event.record()
         with torch.cuda.stream(self.stream):
             self.stream.wait_event(event)
-            for lo, hi, work in self._held:
+            for b, lo, hi, work in self._held:
                 if work is not None:
                     work.wait()  # update stream waits for the bucket's all-reduce
                 for fence in self.pre_update_fences:
                     fence()
-                self._update_range(lo, hi)
-                self._done_ranges.append((lo, hi))
+                self._update_bucket(b, lo, hi)
         self._held = []
+
+    # --- sharded optimizer (GradReducer(shard=True), --shard-optimizer) ----------------------
+    def _sharded(self) -> bool:
+        r = getattr(self, "reducer", None) or getattr(self.flat, "reducer", None)
+        return bool(r is not None and r.shard)
+
+    def _update_bucket(self, b, lo, hi, coeffs=None):
+        """Update bucket b's parameters this rank owns, then (sharded) all-gather them, issued on the
+        current stream behind the update."""
+        r = getattr(self.flat, "reducer", None)
+        if r is None or not r.shard:
+            self._update_range(lo, hi, coeffs)
+            self._done_ranges.append((lo, hi))
+            return
+        for a, z in r.owned(b):
+            self._update_range(a, z, coeffs)
+            self._done_ranges.append((a, z))
+        self._gathers.extend(r.gather_params(b))
+
+    def _finish_gathers(self):
+        """The current stream waits for the parameter all-gathers; the transposed shadows are then
+        re-derived from the gathered parameters."""
+        if not self._gathers and not self._sharded():
+            return
+        for w in self._gathers:
+            w.wait()
+        self._gathers = []
+        self.flat.refresh_transposed()
+
+    def gather_state(self):
+        """Collective (sharded optimizer): all-gather the moments (and the fp32 master) so every rank
+        holds the full optimizer state, as a checkpoint stores it. A no-op otherwise."""
+        r = getattr(self.flat, "reducer", None)
+        if r is None or not r.shard:
+            return
+        if self.overlap and self.stream is not None:
+            torch.cuda.current_stream(self.flat.data.device).wait_stream(self.stream)
+        ts = [self.exp_avg, self.exp_avg_sq] + ([self.master] if self.master is not None else [])
+        works = [w for b in range(r.num_buckets) for w in r.gather_params(b, ts)]
+        for w in works:
+            w.wait()
 
     def _bind_state(self):
         for p in self.param_groups[0]["params"]:
@@ -251,6 +299,7 @@ class FlatAdamW(torch.optim.AdamW):
             self.release_held()
             if self.stream is not None:
                 torch.cuda.current_stream(self.flat.data.device).wait_stream(self.stream)
+            self._finish_gathers()
             self._in_step = False
             self._done_ranges = []
             return loss
@@ -261,7 +310,15 @@ class FlatAdamW(torch.optim.AdamW):
         lr, eps, wd = float(g["lr"]), float(g["eps"]), float(g["weight_decay"])
         bc1 = 1.0 - b1 ** self._step
         bc2_sqrt = math.sqrt(1.0 - b2 ** self._step)
-        self._update_range(0, self.flat.numel, (lr, b1, b2, eps, wd, bc1, bc2_sqrt))
+        coeffs = (lr, b1, b2, eps, wd, bc1, bc2_sqrt)
+        r = getattr(self.flat, "reducer", None)
+        if r is not None and r.shard:
+            for b, (lo, hi) in enumerate(r.ranges):
+                self._update_bucket(b, lo, hi, coeffs)
+            self._done_ranges = []
+            self._finish_gathers()
+            return loss
+        self._update_range(0, self.flat.numel, coeffs)
         return loss
 
     def _step_reference(self, lr, b1, b2, eps, wd, bc1, bc2_sqrt, lo=0, hi=None):
@@ -289,6 +346,13 @@ class FlatAdamW(torch.optim.AdamW):
         vd.copy_(v)
 
     # --- checkpoint compatibility -------------------------------------------------------
+    def checkpoint_bytes(self) -> int:
+        """Tensor bytes a checkpoint of this model + optimizer holds: the parameters, both moments
+        and (``--master-weights fp32``) the fp32 master -- 6 B/param pure bf16, 14 B/param with the
+        master. Sizes the time-aware final-save estimate and the pinned staging pool."""
+        n = self.flat.data.nbytes + self.exp_avg.nbytes + self.exp_avg_sq.nbytes
+        return n + (self.master.nbytes if self.master is not None else 0)
+
     def state_dict(self):
         for st in self.state.values():
             st["step"] = torch.tensor(float(self._step), dtype=torch.float32)

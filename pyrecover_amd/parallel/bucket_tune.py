@@ -81,22 +81,87 @@ def probe_allreduce(device: torch.device, dtype: torch.dtype = torch.bfloat16, s
     return out
 
 
+class _ProbeFlat:
+    """The part of FlatParams the xGMI engine touches: a gradient buffer it may re-point."""
+
+    def __init__(self, n: int, dtype: torch.dtype, device: torch.device):
+        self.grad = torch.zeros(n, dtype=dtype, device=device)
+
+    def rebind_grad(self, new: torch.Tensor):
+        self.grad = new
+
+
+def probe_xgmi(device: torch.device, dtype: torch.dtype = torch.bfloat16, sizes_mb: Sequence[int] = PROBE_MB,
+               iters: int = 3, group=None) -> List[Tuple[float, float]]:
+    """probe_allreduce through the direct xGMI engine (parallel/xgmi.py): one single-bucket engine per
+    probe size over a scratch buffer, timed launch -> wait -> end_step, MAX over ranks. Collective."""
+    from .xgmi import XgmiAllReduce
+
+    esz = torch.empty((), dtype=dtype).element_size()
+    out = []
+    for mb in sizes_mb:
+        n = mb * 2 ** 20 // esz
+        eng = XgmiAllReduce(_ProbeFlat(n, dtype, device), [(0, n)], group)
+
+        def once():
+            eng.launch(0).wait()
+            eng.end_step()
+
+        once()
+        torch.cuda.synchronize(device)
+        dist.barrier(group=group)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            once()
+        torch.cuda.synchronize(device)
+        dt = torch.tensor([(time.perf_counter() - t0) / iters], dtype=torch.float64, device=device)
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX, group=group)
+        out.append((float(n * esz), float(dt.item())))
+        del eng
+    return out
+
+
+def _summary(samples, world) -> dict:
+    alpha, beta = fit_latency_bandwidth(samples)
+    return {"alpha_us": round(alpha * 1e6, 1),
+            "algbw_gbps": None if beta == float("inf") else round(beta / 1e9, 2),
+            "busbw_gbps": None if beta == float("inf") else round(beta / 1e9 * 2 * (world - 1) / world, 2),
+            "probe": [{"mb": round(b / 2 ** 20), "ms": round(t * 1e3, 3)} for b, t in samples]}
+
+
 def autotune_bucket_mb(device: torch.device, dtype: torch.dtype = torch.bfloat16, group=None,
-                       sizes_mb: Sequence[int] = PROBE_MB, iters: int = 3, overhead: float = 0.1) -> Tuple[int, dict]:
-    """Probe, fit and choose; returns (bucket MiB, report). Single process: the 256 MiB default."""
+                       sizes_mb: Sequence[int] = PROBE_MB, iters: int = 3, overhead: float = 0.1,
+                       backend: str = "rccl", flat=None) -> Tuple[int, dict]:
+    """Probe, fit and choose; returns (bucket MiB, report). Single process: the 256 MiB default.
+
+    RCCL is always probed. On a GPU group the xGMI engine is probed too (``backend="xgmi"``: the
+    bucket size is chosen from ITS fit; otherwise it is reported next to RCCL's, and a probe that
+    cannot run -- e.g. per-task GPU isolation -- is reported as such), so the first multi-GPU run logs
+    both bus bandwidths."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) < 2:
         return 256, {"world": 1, "chosen_mb": 256}
+    world = dist.get_world_size(group)
     samples = probe_allreduce(device, dtype, sizes_mb, iters, group)
-    alpha, beta = fit_latency_bandwidth(samples)
+    report = {"world": world, "rccl": _summary(samples, world)}
+    chosen_from = samples
+    if device.type == "cuda":
+        try:
+            xs = probe_xgmi(device, dtype, sizes_mb, iters, group)
+            report["xgmi"] = _summary(xs, world)
+            if backend == "xgmi":
+                chosen_from = xs
+        except Exception as e:  # noqa: BLE001 - decided collectively inside XgmiAllReduce (raises on all ranks)
+            if backend == "xgmi":
+                raise
+            report["xgmi"] = f"not available: {str(e).splitlines()[0][:160]}"
+    alpha, beta = fit_latency_bandwidth(chosen_from)
     mb = choose_bucket_mb(alpha, beta, overhead)
     choice = torch.tensor([mb], dtype=torch.int64, device=device if device.type == "cuda" else "cpu")
     dist.broadcast(choice, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
     mb = int(choice.item())
-    world = dist.get_world_size(group)
-    report = {"world": world, "chosen_mb": mb, "alpha_us": round(alpha * 1e6, 1),
-              "algbw_gbps": None if beta == float("inf") else round(beta / 1e9, 2),
-              "busbw_gbps": None if beta == float("inf") else round(beta / 1e9 * 2 * (world - 1) / world, 2),
-              "probe": [{"mb": round(b / 2 ** 20), "ms": round(t * 1e3, 3)} for b, t in samples]}
+    report.update({"chosen_mb": mb, "chosen_for": backend if device.type == "cuda" else "rccl",
+                   "alpha_us": report["rccl"]["alpha_us"], "busbw_gbps": report["rccl"]["busbw_gbps"],
+                   "probe": report["rccl"]["probe"]})
     return mb, report
 
 

@@ -19,7 +19,21 @@ import torch
 
 logger = logging.getLogger("pyrecover")
 
-_STATE = {"rank": 0, "world": 1, "local_rank": 0, "initialized": False, "backend": None}
+_STATE = {"rank": 0, "world": 1, "local_rank": 0, "initialized": False, "backend": None, "reducer": None}
+
+
+def set_reducer_settings(bucket_mb=None, allreduce=None, shard_optimizer=None, sparse_embedding=None):
+    """Record how this run splits and reduces gradients (bucket size in MiB, all-reduce backend,
+    sharded optimizer, sparse embedding exchange): bucket boundaries decide how RCCL splits each
+    message and so the order in which an element's W contributions are summed. Recorded in every
+    checkpoint (``pyrecover_state.reduction``) and compared on resume. Replaces what an earlier
+    call recorded (one training run per call)."""
+    cur = {}
+    for k, v in (("bucket_mb", bucket_mb), ("allreduce", allreduce), ("shard_optimizer", shard_optimizer),
+                 ("sparse_embedding", sparse_embedding)):
+        if v is not None:
+            cur[k] = v
+    _STATE["reducer"] = cur
 
 
 def is_distributed_slurm_env() -> bool:
@@ -141,7 +155,13 @@ def rccl_order_settings(environ=None) -> dict:
     out = {k: env[k] for k in RCCL_ORDER_KEYS if k in env}
     out["world_size"] = get_world_size() if _STATE.get("initialized") else 1
     out["backend"] = _STATE.get("backend") or "none"
+    out["rccl_order_pinned"] = env.get("PYRECOVER_RCCL_DETERMINISTIC", "0") == "1"
+    for k, v in (_STATE.get("reducer") or {}).items():
+        out[k] = v
     return out
+
+
+_NEWER_KEYS = ("rccl_order_pinned", "bucket_mb", "allreduce", "shard_optimizer", "sparse_embedding")
 
 
 def compare_rccl_order(saved: Optional[dict], current: Optional[dict] = None) -> list:
@@ -151,7 +171,8 @@ def compare_rccl_order(saved: Optional[dict], current: Optional[dict] = None) ->
     if not saved:
         return []
     cur = rccl_order_settings() if current is None else current
-    keys = sorted(set(saved) | set(cur))
+    # keys a checkpoint of an older version does not carry are not differences
+    keys = sorted(k for k in set(saved) | set(cur) if k in saved or k not in _NEWER_KEYS)
     return [f"{k}: saved {saved.get(k, '<unset>')!r}, now {cur.get(k, '<unset>')!r}" for k in keys
             if saved.get(k) != cur.get(k)]
 

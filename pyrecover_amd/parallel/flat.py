@@ -32,7 +32,7 @@ ALIGN = 64  # elements; every group starts 128-B aligned for bf16 (16-B vector l
 
 
 class GradSlot:
-    __slots__ = ("flat", "index", "params", "offset", "numel", "view", "fresh", "bucket", "fused")
+    __slots__ = ("flat", "index", "params", "offset", "numel", "view", "fresh", "bucket", "fused", "sparse_ids")
 
     def __init__(self, flat, index, params, offset, numel, fused):
         self.flat = flat
@@ -44,6 +44,7 @@ class GradSlot:
         self.fresh = True
         self.bucket = -1
         self.fused = fused
+        self.sparse_ids = None  # token ids behind an embedding gradient (sparse exchange, parallel/ddp.py)
 
     # --- producers ------------------------------------------------------------------
     def mm_(self, a: torch.Tensor, b: torch.Tensor, shape: Tuple[int, int]):
@@ -114,6 +115,58 @@ class FlatParams:
                 for p in slot.params:
                     self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(slot)))
         self._pending_unfused: Dict[int, int] = {}
+
+    # --- layout for the sharded optimizer -------------------------------------------------
+    def relayout(self, buckets: Sequence[Sequence[int]], multiple: int) -> List[Tuple[int, int]]:
+        """Re-place the fusion groups so every bucket (a list of consecutive slot indices) spans a
+        multiple of ``multiple`` elements, zero padding after its last group; returns the buckets'
+        new [lo, hi) ranges, indexed like ``buckets``. The sharded reducer uses it so each bucket
+        splits into W equal chunks with no remainder: its reduce-scatter then covers the bucket
+        exactly as the all-reduce would (same chunking, same summation order). Parameter values
+        move with their groups; call before an optimizer is bound to the buffers."""
+        if getattr(self, "layout_frozen", False):
+            raise RuntimeError("relayout after an optimizer was bound to the flat buffers")
+        order = sorted(range(len(buckets)), key=lambda b: min(buckets[b]))
+        new_off: Dict[int, int] = {}
+        ranges: List[Tuple[int, int]] = [(0, 0)] * len(buckets)
+        off = 0
+        for b in order:
+            start = off = (off + ALIGN - 1) // ALIGN * ALIGN
+            for gi in sorted(buckets[b]):
+                off = (off + ALIGN - 1) // ALIGN * ALIGN
+                new_off[gi] = off
+                off += self.slots[gi].numel
+            off = start + -(-(off - start) // multiple) * multiple
+            ranges[b] = (start, off)
+        if sorted(new_off) != list(range(len(self.slots))):
+            raise ValueError("relayout: every slot must be in exactly one bucket")
+        numel = (off + ALIGN - 1) // ALIGN * ALIGN
+        data = torch.zeros(numel, dtype=self.dtype, device=self.device)
+        grad = torch.zeros(numel, dtype=self.dtype, device=self.device)
+        old_of = {s.index: s.offset for s in self.slots}
+        with torch.no_grad():
+            for s in self.slots:
+                o, n = new_off[s.index], s.numel
+                data[o:o + n].copy_(self.data[old_of[s.index]:old_of[s.index] + n])
+                grad[o:o + n].copy_(self.grad[old_of[s.index]:old_of[s.index] + n])
+        shift = {}
+        for s in self.slots:
+            shift[s.index] = new_off[s.index] - old_of[s.index]
+            s.offset = new_off[s.index]
+            s.view = grad[s.offset:s.offset + s.numel]
+        for p in self.params:
+            s = self.slot_of[id(p)]
+            o = self.param_offset[id(p)] + shift[s.index]
+            self.param_offset[id(p)] = o
+            p.data = data[o:o + p.numel()].view_as(p)
+            p.grad = grad[o:o + p.numel()].view_as(p)
+        self.data, self.grad, self.numel = data, grad, numel
+        if getattr(self, "t_mats", None):
+            by_old = {old_of[s.index]: s.index for s in self.slots}
+            self.t_mats = sorted((o + shift[by_old[o]] if o in by_old else o, r, c) for o, r, c in self.t_mats)
+            self.t_index = {m[0]: i for i, m in enumerate(self.t_mats)}
+            self.data_t = None
+        return ranges
 
     # --- views ----------------------------------------------------------------------
     def weight(self, params: Sequence[torch.nn.Parameter], shape: Tuple[int, int]) -> torch.Tensor:

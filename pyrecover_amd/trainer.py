@@ -219,21 +219,39 @@ def train(args):
     with set_default_dtype(model_dtype), torch.device(device):
         model = Transformer(model_config)
     model.activation_checkpointing = bool(getattr(args, "activation_checkpointing", False))
-    flat = model.flatten_(tokens_per_step=local_batch_size * seq_len)
+    shard = bool(getattr(args, "shard_optimizer", False)) and is_dist
+    # the sharded optimizer's owned chunks cut matrices: no transposed weight shadows (each would be
+    # re-derived from the gathered parameters every step)
+    flat = model.flatten_(tokens_per_step=local_batch_size * seq_len, shadows=False if shard else None)
     overlap = not (args.clip_grad or args.no_overlap_optimizer)
     reducer = None
     if is_dist:
         broadcast_flat(flat)
     bucket_mb = args.bucket_cap_mb
+    if bucket_mb == "auto" and is_dist and args.resume_from_checkpoint is not None:
+        # a resumed run keeps the bucket layout it was checkpointed with: bucket boundaries decide
+        # how every element's contributions are summed (bit-exact resume)
+        saved = ckcore.peek_reduction(args.resume_from_checkpoint, exp_dir=Path(args.checkpoint_dir) /
+                                      args.experiment_name, distributed=args.use_torch_distributed_ckpt)
+        if saved and saved.get("bucket_mb"):
+            bucket_mb = float(saved["bucket_mb"])
+            log_rank0(f"Bucket size {bucket_mb} MiB from the checkpoint (--bucket-cap-mb auto, resume)")
     if bucket_mb == "auto":
         from .parallel.bucket_tune import autotune_bucket_mb
 
-        bucket_mb, tune = autotune_bucket_mb(device, flat.grad.dtype) if is_dist else (256.0, {"world": 1})
+        bucket_mb, tune = (autotune_bucket_mb(device, flat.grad.dtype, backend=args.allreduce, flat=flat)
+                           if is_dist else (256.0, {"world": 1}))
         log_rank0(f"Bucket autotune: {bucket_mb} MiB {tune}")
+    sparse_emb = _use_sparse_embedding(getattr(args, "sparse_embedding_grad", "off"), world_size,
+                                       local_batch_size * seq_len * accum, vocab)
     if is_dist or overlap:
-        reducer = GradReducer(flat, bucket_cap_mb=bucket_mb, backend=args.allreduce)
+        reducer = GradReducer(flat, bucket_cap_mb=bucket_mb, backend=args.allreduce, shard=shard,
+                              sparse_slot=flat.slot(model.tok_embeddings.weight).index if sparse_emb else None)
         log_rank0(f"Gradient buckets: {reducer.num_buckets}, {sum(reducer.bucket_bytes()) / 2**30:.2f} GiB"
-                  f"{' (RCCL all-reduce)' if is_dist else ''}")
+                  f"{(' (RCCL reduce-scatter + all-gather, sharded optimizer)' if shard else ' (RCCL all-reduce)') if is_dist else ''}"
+                  f"{', sparse embedding-gradient exchange' if sparse_emb and is_dist else ''}")
+    D.set_reducer_settings(bucket_mb=float(bucket_mb) if is_dist else None, allreduce=args.allreduce if is_dist else None,
+                           shard_optimizer=shard, sparse_embedding=bool(sparse_emb and is_dist))
     model.train()
     # SUM all-reduce of `accum` summed micro-batch gradients: the mean is folded into the update
     grad_scale = 1.0 / (world_size * accum)
@@ -259,7 +277,7 @@ def train(args):
             from .graph import StepGraph
 
             pre = (lambda: setattr(optimizer, "grad_scale_dev",
-                                   _clip_coef(flat, args.grad_max_norm, grad_scale))) if args.clip_grad else None
+                                   _clip_coef(flat, args.grad_max_norm, grad_scale, reducer))) if args.clip_grad else None
             step_graph = StepGraph(model, optimizer, reducer, fences=[ckcore.fence_all], pre_step=pre)
             log_rank0(f"--compile: the training step is captured into a HIP graph after "
                       f"{args.compile_warmup_steps} eager steps and replayed (no Inductor/Triton)")
@@ -275,7 +293,7 @@ def train(args):
         # Allocated now, while the GPU is idle: hipHostMalloc maps the pool into the GPU's page
         # tables, and doing that under running kernels (a background thread during the first
         # steps) was measured at 150 s for 11 GB instead of ~2 s.
-        est = 3 * flat.numel * flat.data.element_size() // (world_size if args.use_torch_distributed_ckpt else 1)
+        est = optimizer.checkpoint_bytes() // (world_size if args.use_torch_distributed_ckpt else 1)
         t0 = time.perf_counter()
         ckcore.Checkpointer.get(device).prewarm(int(est * 1.05) + (64 << 20), background=False)
         log_rank0(f"Pinned checkpoint staging pool: {est / 2**30:.2f} GiB in {time.perf_counter() - t0:.2f}s")
@@ -346,8 +364,9 @@ def train(args):
     if stopper is not None:
         if is_dist:
             stopper.extra_iters = 1  # every rank acts on rank 0's decision one step later (_StopFlagSync)
-        # what the final save writes on this rank: bf16/fp32 params + AdamW m, v (+ small entries)
-        state_bytes = 3 * flat.state_bytes()
+        # what the final save writes on this rank: params + AdamW m, v (+ the fp32 master with
+        # --master-weights fp32: 14 instead of 6 B/param) (+ small entries)
+        state_bytes = optimizer.checkpoint_bytes()
         if args.use_torch_distributed_ckpt:
             state_bytes = -(-state_bytes // world_size)
         inline_md5 = bool(args.verify_checkpoints) and not args.use_torch_distributed_ckpt
@@ -385,6 +404,9 @@ def train(args):
         log_rank0(f"Checkpoint loading completed in {dt:.2f} seconds")
     D.barrier()
 
+    # cross-rank replica check (parallel/consistency.py): every N steps and at the end
+    check_every = args.replica_check_every if getattr(args, "replica_check_every", None) is not None \
+        else 10 * max(1, int(args.logging_frequency))
     train_dl_iterator = iter(train_dl)
     should_stop = False
     local_stop = False  # rank 0's own time decision (latched; acted on via the broadcast when W > 1)
@@ -456,7 +478,7 @@ def train(args):
             if reducer is not None:
                 reducer.finish()
             if args.clip_grad:
-                optimizer.grad_scale_dev = _clip_coef(flat, args.grad_max_norm, grad_scale)
+                optimizer.grad_scale_dev = _clip_coef(flat, args.grad_max_norm, grad_scale, reducer)
             ckcore.fence_all()  # an async snapshot must land before parameters change
             optimizer.step()
             eager_steps_this_run += 1
@@ -492,6 +514,9 @@ def train(args):
             ntokens_since_last_log = 0
             ntraining_tokens_since_last_log = 0
             time_last_log = time.perf_counter()
+
+        if is_dist and check_every > 0 and train_step % check_every == 0:
+            _replica_check(flat, optimizer, train_step)
 
         dev_step = step_timer.record()
         if stopper is not None:
@@ -543,7 +568,8 @@ def train(args):
 
     # drain background checkpoint writes (and deferred .md5 digests) before reporting; after a
     # time-aware stop the digests get only the time left before the wall-clock limit (minus a
-    # margin; 60 s after a signal) -- one cut short leaves no .md5, and .md5parts verify the resume
+    # margin; 60 s after a signal) -- a checkpoint of this job whose digest was cut short has no
+    # .md5; with --verify-checkpoints it is removed below (the final checkpoint supersedes it)
     if stop_sync is not None:
         stop_sync.collect()  # retire the last posted broadcast before teardown
     t0 = time.perf_counter()
@@ -562,6 +588,8 @@ def train(args):
     else:
         ckcore.flush_all()
     total_checkpoint_store_time += time.perf_counter() - t0
+    if is_dist and check_every > 0 and loss is not None:
+        _replica_check(flat, optimizer, train_step)
     total_training_time = time.perf_counter() - training_start_time
     if csv_file is not None:
         csv_file.close()
@@ -617,11 +645,54 @@ def _diagnostics(step_timer, device, comm_timer, world_size, ckpt_window, stoppe
     return out
 
 
-def _clip_coef(flat, max_norm: float, pre_scale: float):
-    """Device-side clip coefficient min(1, max_norm / ||g||) over the flat (reduced) gradient."""
+def _clip_coef(flat, max_norm: float, pre_scale: float, reducer=None):
+    """Device-side clip coefficient min(1, max_norm / ||g||) over the flat (reduced) gradient. With
+    the sharded optimizer each rank holds only its chunks reduced: the squared norms of those (the
+    shared tails counted on rank 0 only) are summed over the ranks."""
     from . import _ext
 
+    if reducer is not None and reducer.shard:
+        ranges = [(a, z) for b in range(reducer.num_buckets) for i, (a, z) in enumerate(reducer.owned(b))
+                  if reducer.rank == 0 or a < reducer.ranges[b][0] + reducer.chunks[b] * reducer.world]
+        parts = []
+        for a, z in ranges:
+            g = flat.grad[a:z]
+            if _ext.hip(g):
+                parts.append(_ext.native().grad_norm(g, max_norm, 1.0)[0:1].double() ** 2)
+            else:
+                parts.append(g.double().pow(2).sum().reshape(1))
+        sq = torch.stack(parts).sum().reshape(1) if parts else torch.zeros(1, dtype=torch.float64,
+                                                                           device=flat.grad.device)
+        torch.distributed.all_reduce(sq, group=reducer.group)
+        norm = sq.sqrt() * pre_scale
+        return torch.clamp(max_norm / (norm + 1e-6), max=1.0).reshape(1).float()
     if _ext.hip(flat.grad):
         return _ext.native().grad_norm(flat.grad, max_norm, pre_scale)[1:2]
     norm = flat.grad.to(torch.promote_types(flat.grad.dtype, torch.float32)).norm() * pre_scale
     return torch.clamp(max_norm / (norm + 1e-6), max=1.0).reshape(1).float()
+
+
+def _replica_check(flat, optimizer, step: int):
+    """Collective: stop when the DDP replicas are no longer identical (parallel/consistency.py)."""
+    from .parallel.consistency import replica_report
+
+    rep = replica_report(flat, optimizer)
+    if rep["mismatched"]:
+        msg = (f"replica check at step {step}: {', '.join(rep['mismatched'])} differ across ranks: "
+               + "; ".join(f"{k}: {rep['checksums'][k]}" for k in rep["mismatched"]))
+        logger.error(msg)
+        raise RuntimeError(msg)
+    log_rank0(f"Replica check at step {step}: parameters"
+              f"{'' if rep['optimizer_identical_across_ranks'] is None else ' and optimizer moments'} identical "
+              f"on all ranks")
+
+
+def _use_sparse_embedding(mode: str, world: int, tokens_per_rank: int, vocab: int) -> bool:
+    """--sparse-embedding-grad: on / off, or auto: W > 1 and the job's tokens per step at most half
+    the vocabulary (then the exchanged rows are at most half of the dense gradient's, which the
+    all-reduce would move twice)."""
+    if mode == "on":
+        return True
+    if mode == "auto":
+        return world > 1 and 2 * world * tokens_per_rank <= vocab
+    return False

@@ -410,9 +410,12 @@ def test_save_cost_probe_and_drop_unverified(tmp_path):
         if md5:
             (tmp_path / f"ckpt_{n}.pt.md5").write_text("0" * 32)
     (tmp_path / "ckpt_5_final.pt").write_bytes(b"x")
-    removed = ck.drop_unverified(tmp_path, str(tmp_path / "ckpt_5_final.pt"))
+    (tmp_path / "ckpt_1.pt").write_bytes(b"x")  # an earlier job's checkpoint, written without a digest
+    mine = {str(tmp_path / f"ckpt_{n}.pt") for n in (2, 4, 6)}  # this process deferred their digests
+    removed = ck.drop_unverified(tmp_path, str(tmp_path / "ckpt_5_final.pt"), only=mine)
     assert [Path(r).name for r in removed] == ["ckpt_4.pt"]
-    assert sorted(p.name for p in tmp_path.glob("*.pt")) == ["ckpt_2.pt", "ckpt_5_final.pt", "ckpt_6.pt"]
+    assert sorted(p.name for p in tmp_path.glob("*.pt")) == ["ckpt_1.pt", "ckpt_2.pt", "ckpt_5_final.pt",
+                                                              "ckpt_6.pt"]
     assert not (tmp_path / "ckpt_4.pt.md5parts").exists()
 
 

@@ -17,17 +17,41 @@ def test_comm_predict_simulate_in_order_stream():
     gb = 1e9
     # two 1 GB buckets, 8 ranks, 100 GB/s bus bandwidth, no latency: each all-reduce takes
     # 2 * 7/8 * 1 GB / 100 GB/s = 17.5 ms; the second waits for the first (in-order stream)
-    exposed, ends = simulate(ready=[10.0, 12.0], bwd_end=20.0, nbytes=[gb, gb], world=8, busbw_gbps=100.0,
-                             latency_us=0.0)
+    exposed, ends, _ = simulate(ready=[10.0, 12.0], bwd_end=20.0, nbytes=[gb, gb], world=8, busbw_gbps=100.0,
+                                latency_us=0.0)
     assert ends == pytest.approx([27.5, 45.0])
     assert exposed == pytest.approx(25.0)
     # a bucket that is ready after the previous one finished starts at its ready time
-    exposed, ends = simulate([0.0, 50.0], 60.0, [gb, gb], 8, 100.0, 0.0)
+    exposed, ends, _ = simulate([0.0, 50.0], 60.0, [gb, gb], 8, 100.0, 0.0)
     assert ends == pytest.approx([17.5, 67.5])
     assert exposed == pytest.approx(7.5)
     # fully hidden: nothing exposed; per-collective latency is added to every bucket
-    exposed, ends = simulate([0.0], 100.0, [gb], 8, 100.0, 1000.0)
+    exposed, ends, _ = simulate([0.0], 100.0, [gb], 8, 100.0, 1000.0)
     assert ends == pytest.approx([18.5]) and exposed == 0.0
+
+
+def test_comm_predict_models_updates_and_sharding():
+    """The AdamW update of a bucket waits for its reduction (in-order side stream) and can be what
+    is exposed; ZeRO-1 halves the reduction's bus bytes, divides the update by N and adds the
+    parameter all-gather on the same FIFO stream (RS_0, RS_1, AG_0, AG_1)."""
+    from comm_predict import simulate
+
+    gb = 1e9
+    # all-reduce 17.5 ms each; updates of 10 ms each (20 ms for the whole model)
+    exp, ends, upd = simulate([10.0, 12.0], 20.0, [gb, gb], 8, 100.0, 0.0, adamw_ms=20.0)
+    assert ends == pytest.approx([27.5, 45.0]) and upd == pytest.approx([37.5, 55.0]) and exp == pytest.approx(35.0)
+    # one GPU: no communication, the updates alone (what the measured 1-GPU step already contains)
+    exp1, _, upd1 = simulate([10.0, 12.0], 20.0, [gb, gb], 1, 1.0, 0.0, adamw_ms=20.0)
+    assert upd1 == pytest.approx([20.0, 30.0]) and exp1 == pytest.approx(10.0)
+    # ZeRO-1: RS 8.75 ms, update 1.25 ms, AG 8.75 ms (behind its update)
+    exp, ends, upd = simulate([10.0, 12.0], 20.0, [gb, gb], 8, 100.0, 0.0, adamw_ms=20.0, mode="shard")
+    # RS_0 10 -> 18.75, u_0 -> 20.0; RS_1 18.75 -> 27.5, u_1 -> 28.75; AG_0 27.5 -> 36.25; AG_1 -> 45.0
+    assert ends == pytest.approx([18.75, 27.5, 36.25, 45.0]) and upd == pytest.approx([20.0, 28.75])
+    assert exp == pytest.approx(25.0)
+    # sparse embedding exchange: the last bucket becomes a small all-gather
+    exp_s, ends_s, _ = simulate([10.0, 12.0], 20.0, [gb, gb], 8, 100.0, 0.0, adamw_ms=20.0,
+                                sparse_bytes=0.1 * gb)
+    assert ends_s[-1] == pytest.approx(27.5 + 0.875) and exp_s < 35.0
 
 
 def _write_trace(path, rows):

@@ -9,7 +9,7 @@ OUT=build_gpu/attn_var
 mkdir -p $OUT
 HIPCC=${ROCM_PATH:-/opt/rocm}/bin/hipcc
 FL="-O3 -std=c++17 --offload-arch=gfx950 -Icsrc -Icsrc/kernels"
-AFL="-fno-honor-nans -fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form"
+AFL=${AFL-"-fno-honor-nans -fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form"}
 [ -f $OUT/attention_f32.o ] || $HIPCC $FL -c csrc/kernels/attention_f32.hip -o $OUT/attention_f32.o
 [ -f $OUT/harness.o -a $OUT/harness.o -nt tools/attn_harness.cpp ] || $HIPCC $FL -c tools/attn_harness.cpp -o $OUT/harness.o
 pids=()
