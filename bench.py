@@ -63,6 +63,9 @@ def parse():
                     help="W > 1: ZeRO-1 (reduce-scatter, 1/W AdamW update, parameter all-gather; train.py flag)")
     ap.add_argument("--sparse-embedding-grad", choices=["auto", "on", "off"], default="auto",
                     help="W > 1: token-embedding gradient as (id, row) pairs (auto: tokens per step <= vocab / 2)")
+    ap.add_argument("--comm-probe", choices=["rccl", "all", "off"], default="rccl",
+                    help="W > 1, after the timed steps: all-reduce probe bus bandwidth on the job's group "
+                         "(rccl; all: also the direct xGMI engine) reported in the JSON line")
     ap.add_argument("--cpu", action="store_true",
                     help="run on the CPU over gloo (tests of the launcher and the DDP path; not a benchmark)")
     ap.add_argument("--gemm-tuning", choices=["auto", "off", "tune"], default="auto",
@@ -106,7 +109,7 @@ def _adamw_fast() -> bool:
 
 def _opt_sched(tokens: int = 0) -> str:
     """Where the overlapped AdamW update runs; `tokens` = B * S of one attention call (the window
-    opens before the dQ kernel at <= 4096 tokens unless PYRECOVER_ATTN_BWD_WINDOW pins it)."""
+    opens before the dQ kernel at <= 4096 tokens unless the attention option bwd_window pins it)."""
     from pyrecover_amd import _ext
     from pyrecover_amd.optim import adamw
 
@@ -265,6 +268,17 @@ def main():
     from pyrecover_amd.parallel.consistency import replica_report
 
     replicas = replica_report(flat, opt)
+    probe = None
+    if world > 1 and args.comm_probe != "off":
+        # after the clock stopped: the group's all-reduce latency / bus bandwidth, measured
+        from pyrecover_amd.parallel import bucket_tune as BT
+
+        probe = {"rccl": BT._summary(BT.probe_allreduce(dev, flat.grad.dtype), world)}
+        if args.comm_probe == "all" and dev.type == "cuda":
+            try:
+                probe["xgmi"] = BT._summary(BT.probe_xgmi(dev, flat.grad.dtype), world)
+            except Exception as e:  # noqa: BLE001 - raised on every rank (XgmiAllReduce decides collectively)
+                probe["xgmi"] = f"not available: {str(e).splitlines()[0][:160]}"
     tokens = B * S * world * args.steps
     tps = tokens / dt
     n_params = model.num_params()
@@ -325,6 +339,7 @@ def main():
         if world > 1:
             out["comm"] = comm
             out["comm_env"] = comm_env()
+            out["comm_probe"] = probe
         if phases:
             n = len(phases)
             out["phase_ms"] = {k: round(sum(e[i].elapsed_time(e[i + 1]) for e in phases) / n, 2)

@@ -833,9 +833,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("checksum", &checksum);
   m.def("wgrad_mm_", &wgrad_mm_);
   m.def("wgrad_mm_exp_", &wgrad_mm_exp_);
-  m.def("wgrad_set_streamk", &pra_wgrad_set_streamk,
-        "weight-gradient schedule: 0 whole tiles + split tail, 1 stream-K when tiles % CUs != 0, 2 always");
-  m.def("wgrad_get_streamk", &pra_wgrad_get_streamk);
   m.def("gemm_nt_", &gemm_nt_, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("epi") = 0,
         py::arg("out2") = py::none(), py::arg("tab") = py::none(), py::arg("S") = 0, py::arg("D") = 0,
         py::arg("nrot") = 0);
@@ -848,10 +845,9 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("dout"), pybind11::arg("lse"), pybind11::arg("dq"), pybind11::arg("dk"), pybind11::arg("dv"),
         pybind11::arg("scale"), pybind11::arg("causal"), pybind11::arg("rope_tab") = pybind11::none(),
         pybind11::arg("mid_event") = 0);
-  m.def("attn_set_order", [](int fwd, int dq, int dkdv, int wave_pair) { pra_attn_set_order(fwd, dq, dkdv, wave_pair); },
-        "block order of the attention forward / dQ / dK/dV grids: 0 = heavy tiles first, G > 0 = XCD-grouped "
-        "with G heads per group, -1 = by shape; wave_pair = 1: long and short row groups share each SIMD",
-        pybind11::arg("fwd"), pybind11::arg("dq"), pybind11::arg("dkdv"), pybind11::arg("wave_pair") = 0);
+  m.def("attn_set_order", [](int fwd, int dq, int dkdv) { pra_attn_set_order(fwd, dq, dkdv); },
+        "block order of the attention grids: 0 = heavy tiles first, G > 0 = XCD-grouped with G heads per group, "
+        "-1 = by shape", pybind11::arg("fwd"), pybind11::arg("dq"), pybind11::arg("dkdv"));
   m.def("attn_set_options", [](int fwd_pipe, double fwd_thr, int dkdv_impl, int dq_pipe, int dkdv_split, int dkdv_kreg,
                                int bwd_fused, int bwd_window) {
     pra_attn_set_options(fwd_pipe, (float)fwd_thr, dkdv_impl, dq_pipe, dkdv_split, dkdv_kreg, bwd_fused, bwd_window);

@@ -82,7 +82,7 @@ template <typename T, bool ACC, int EXP = 0>
 __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, const T* __restrict__ B,
                                                       T* __restrict__ C, int M, int N, int K, long lda, long ldb,
                                                       long ldc, float* __restrict__ ws, int* __restrict__ tickets,
-                                                      int n_split, int S, int skG = 0) {
+                                                      int n_split, int S) {
   __shared__ __attribute__((aligned(1024))) T smem[NS * 2 * TILE];
   const int tiles_m = M / BM, tiles_n = N / BN, nwg = tiles_m * tiles_n, nk = K / BK;
 
@@ -301,70 +301,6 @@ __global__ __launch_bounds__(NTH) void wgrad16_kernel(const T* __restrict__ A, c
       for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   };
 
-  if (skG > 0) {
-    // Persistent data-parallel rounds + a stream-K remainder (skG workgroups, one per CU):
-    //  * all but the last round's worth of whole tiles run as data-parallel rounds, every workgroup
-    //    one tile per round in the classic XCD-aware group-M order (the tiles resident together
-    //    share A/B panels in L2);
-    //  * the remaining skG + nwg % skG tiles' (tile, k-step) iterations are cut into skG equal
-    //    ranges, so every CU ends at the same time however nwg divides by the CU count. A tile
-    //    covered by several ranges is summed deterministically: each range writes its fp32 partial
-    //    to its own slot (2 g: the range's first tile, 2 g + 1: its last), and the last arriver adds
-    //    the partials in range order -- the k order -- whoever arrives last.
-    // (Stream-K over ALL tiles spreads the concurrently active tiles over the whole matrix and lost
-    // 35-40% to L2 misses on the 7B W1|W3 / W2 shapes: profiles/r5/wgrad_bench_7b.log.)
-    const int rem = nwg % skG;
-    const int sk_tiles = rem == 0 ? 0 : min(nwg, skG + rem);
-    const int dp_tiles = nwg - sk_tiles;  // a multiple of skG
-    for (int lin0 = 0; lin0 < dp_tiles; lin0 += skG) {
-      long m0, n0;
-      tile_origin(lin0 + xcd_remap(blockIdx.x, skG), tiles_m, tiles_n, m0, n0);
-      run(m0, n0, 0, nk);
-      store_c(m0, n0);
-    }
-    if (sk_tiles == 0) return;
-    const long W = (long)sk_tiles * nk;
-    const int g = xcd_remap(blockIdx.x, skG);  // consecutive ranges (adjacent tiles) share an XCD
-    auto start = [&](int gg) -> long { return W * gg / skG; };
-    auto owner = [&](long x) -> int {  // the range containing iteration x
-      int gg = (int)(x * skG / W);
-      while (gg + 1 < skG && start(gg + 1) <= x) ++gg;
-      while (gg > 0 && start(gg) > x) --gg;
-      return gg;
-    };
-    long s = start(g);
-    const long e = start(g + 1);
-    const int first_tile = (int)(s / nk);
-    while (s < e) {
-      const int t = (int)(s / nk), kb = (int)(s % nk);  // t: index among the stream-K tiles
-      const int ke = (int)min((long)nk, (long)kb + (e - s));
-      long m0, n0;
-      tile_origin(dp_tiles + t, tiles_m, tiles_n, m0, n0);
-      run(m0, n0, kb, ke);
-      if (kb == 0 && ke == nk) {
-        store_c(m0, n0);
-      } else {
-        put_partial(2L * g + (t == first_tile ? 0 : 1));
-        // the ranges on this tile: the non-empty ones between the owners of its first and last
-        // iteration (with fewer iterations than workgroups, empty ranges sit in between)
-        const int glo = owner((long)t * nk), ghi = owner((long)(t + 1) * nk - 1);
-        int nseg = 0;
-        for (int gg = glo; gg <= ghi; ++gg) nseg += start(gg + 1) > start(gg);
-        if (arrive(tickets + t, nseg)) {
-          zero_acc();
-          for (int gg = glo; gg <= ghi; ++gg) {
-            if (start(gg + 1) <= start(gg)) continue;
-            const bool gfirst = (int)(start(gg) / nk) == t;
-            add_partial(2L * gg + (gfirst ? 0 : 1));
-          }
-          store_c(m0, n0);
-        }
-      }
-      s += ke - kb;
-    }
-    return;
-  }
-
   const int ndp = nwg - n_split;  // whole tiles first, then n_split tiles x S split units
   const bool split = (int)blockIdx.x >= ndp;
   int lin, k0 = 0, k1 = nk, part = 0, st = 0;
@@ -403,18 +339,10 @@ __global__ __launch_bounds__(256) void zero_i32_kernel(int* __restrict__ p, int 
 }  // namespace wg
 }  // namespace pra
 
-namespace {
-// Stream-K scheduling of the weight-gradient GEMM (pra_wgrad_set_streamk): 0 = whole tiles plus the
-// split partial last round (default), 1 = stream-K over one workgroup per CU for every shape whose
-// tile count is not a multiple of the CU count, 2 = stream-K for every shape.
-int g_wg_streamk = 0;
-bool use_streamk(int nwg, int cus) { return g_wg_streamk == 2 || (g_wg_streamk == 1 && nwg % cus != 0); }
-}  // namespace
-
+// (A deterministic stream-K schedule -- persistent data-parallel rounds plus a stream-K remainder --
+// was correct but slower on every shape measured, the concurrently active tiles losing L2 reuse:
+// profiles/r5/wgrad_bench_7b*.log, wgrad_bench_8b_b1.log. Removed in round 6.)
 extern "C" {
-
-void pra_wgrad_set_streamk(int mode) { g_wg_streamk = mode; }
-int pra_wgrad_get_streamk() { return g_wg_streamk; }
 
 // C[M][N] (+)= A^T B with A [K][M] (row stride lda), B [K][N] (row stride ldb), C row stride ldc.
 // ws / tickets: sized by pra_wgrad_ws_floats / pra_wgrad_ticket_count (the split tail; both may be
@@ -423,14 +351,12 @@ int pra_wgrad_get_streamk() { return g_wg_streamk; }
 long pra_wgrad_ws_floats(int M, int N, int K, int cus) {
   using namespace pra::gm;
   const int nwg = (M / BM) * (N / BN);
-  if (use_streamk(nwg, cus)) return 2L * cus * BM * BN;  // two partial slots per workgroup
   const int S = pra::gemm_tail_split(nwg, cus, K / BK, PRA_WG_SMAX);
   return S > 1 ? (long)(nwg % cus) * S * BM * BN : 0;
 }
 int pra_wgrad_ticket_count(int M, int N, int K, int cus) {
   using namespace pra::gm;
   const int nwg = (M / BM) * (N / BN);
-  if (use_streamk(nwg, cus)) return nwg;  // one ticket per tile
   return pra::gemm_tail_split(nwg, cus, K / BK, PRA_WG_SMAX) > 1 ? nwg % cus : 0;
 }
 
@@ -440,26 +366,6 @@ hipError_t pra_wgrad_gemm(int dtype, const void* A, const void* B, void* C, int 
   if (M % BM || N % BN || K % BK || K <= 0 || lda % 8 || ldb % 8 || ldc % 8 || cus <= 0) return hipErrorInvalidValue;
   if ((long)(BK - 1) * lda + M > 0x7fffffffL || (long)(BK - 1) * ldb + N > 0x7fffffffL) return hipErrorInvalidValue;
   const int nwg = (M / BM) * (N / BN);
-  if (use_streamk(nwg, cus) && ws && tickets) {
-    hipLaunchKernelGGL(pra::wg::zero_i32_kernel, dim3((nwg + 255) / 256), dim3(256), 0, s, tickets, nwg);
-    const dim3 grid(cus), block(NTH);
-#define PRA_WG_SK(TT)                                                                                        \
-    if (accumulate)                                                                                          \
-      hipLaunchKernelGGL((pra::wg::wgrad16_kernel<TT, true>), grid, block, 0, s, (const TT*)A, (const TT*)B,   \
-                         (TT*)C, M, N, K, lda, ldb, ldc, ws, tickets, 0, 1, cus);                          \
-    else                                                                                                     \
-      hipLaunchKernelGGL((pra::wg::wgrad16_kernel<TT, false>), grid, block, 0, s, (const TT*)A, (const TT*)B,  \
-                         (TT*)C, M, N, K, lda, ldb, ldc, ws, tickets, 0, 1, cus);
-    if (dtype == pra::kBF16) {
-      PRA_WG_SK(__bf16)
-    } else if (dtype == pra::kF16) {
-      PRA_WG_SK(_Float16)
-    } else {
-      return hipErrorInvalidValue;
-    }
-#undef PRA_WG_SK
-    return hipGetLastError();
-  }
   // split the tiles of a partial last round S ways over K (S <= 2; 7B shapes: W13's 96 tail tiles
   // S = 2, 1.31 -> 1.40 PF; W2's 176 would need S = 4, measured slower, so unsplit)
   const int Sx = pra::gemm_tail_split(nwg, cus, K / BK, PRA_WG_SMAX);

@@ -44,10 +44,6 @@ hipError_t pra_wgrad_gemm_exp(const void* A, const void* B, void* C, int M, int 
                               long ldc, int exp, hipStream_t s);
 long pra_wgrad_ws_floats(int M, int N, int K, int cus);
 int pra_wgrad_ticket_count(int M, int N, int K, int cus);
-// weight-gradient tile schedule: 0 = whole tiles + split partial last round, 1 = stream-K where the
-// tile count is not a multiple of the CU count, 2 = stream-K always (gemm_wgrad.hip)
-void pra_wgrad_set_streamk(int mode);
-int pra_wgrad_get_streamk();
 // C = A B^T, A [M][K], B [N][K] (both K-contiguous) with a fused epilogue (gemm_nt.hip):
 // epi 0 plain, 1 SwiGLU forward (C = gu [M][2F], c2 = a [M][F]), 2 SwiGLU backward in place over
 // gu (C), 3 RoPE on the first nrot columns (tab float2 [S][D/2])
@@ -98,9 +94,8 @@ hipError_t pra_attn_bwd(int dtype, const void* q, const void* k, const void* v, 
 void pra_attn_set_options(int fwd_pipe, float fwd_thr, int dkdv_impl, int dq_pipe, int dkdv_split, int dkdv_kreg,
                           int bwd_fused, int bwd_window);
 // block order of the forward / dQ / dK/dV grids: 0 = heavy tiles first, G > 0 = XCD-grouped with G heads
-// per group, -1 = by shape (attention.hip block_tile); wave_pair = 1 pairs long and short row groups
-// on each SIMD of an 8-wave block (wave_group)
-void pra_attn_set_order(int fwd, int dq, int dkdv, int wave_pair);
+// per group, -1 = by shape (attention.hip block_tile)
+void pra_attn_set_order(int fwd, int dq, int dkdv);
 // fused dQ/dK/dV backward (attention_bwd_fused.hip); ws: 2 B Hq S row constants + B Hq S 128 dQ partials
 hipError_t pra_attn_bwd_fused(int dtype, const void* q, const void* k, const void* v, const void* o, const void* dout,
                               const float* lse, float* ws, void* dq, void* dk, void* dv, int B, int S, int Hq,

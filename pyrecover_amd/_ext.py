@@ -17,7 +17,7 @@ def native():
     global _C, _err
     if _C is not None:
         return _C
-    env = _attn_env()  # a malformed PYRECOVER_ATTN_* raises ValueError naming it, not a load error
+    env = _attn_env()  # a malformed PYRECOVER_ATTN_BWD_FUSED raises ValueError naming it, not a load error
     try:
         import torch  # noqa: F401  (loads torch's HIP runtime first; our .so binds to it)
         from pyrecover_amd import _C as mod
@@ -65,29 +65,29 @@ def hip16(t) -> bool:
 
 
 # Attention kernel selection (csrc/kernels/attention.hip AttnOptions): -1 = by shape. The launchers
-# read no environment; PYRECOVER_ATTN_{FWD_PIPE,FWD_THR,DKDV_IMPL,DQ_PIPE,DKDV_SPLIT,DKDV_KREG,...} are read once
-# here, when the extension loads, and set_attn_options() changes them between launches (tests, A/B tools).
+# read no environment. set_attn_options() changes the options between launches (tests, A/B tools);
+# of the environment only PYRECOVER_ATTN_BWD_FUSED (the one experimental kernel path: the fused
+# deterministic backward) is read, once, when the extension loads -- every other option is a
+# measured by-shape default (docs/KNOBS.md).
 # *_order: block order of the forward / dQ / dK/dV grids (attention.hip block_tile): -1 = XCD-grouped
 # by shape, 0 = heavy tiles first across the grid, G = XCD-grouped with G heads per group.
 _ATTN_DEFAULTS = {"fwd_pipe": -1, "fwd_thr": 8.0, "dkdv_impl": -1, "dq_pipe": -1, "dkdv_split": 1, "dkdv_kreg": -2,
                   "bwd_fused": 0, "bwd_window": -1, "fwd_order": -1, "dq_order": -1, "dkdv_order": -1,
-                  "wave_pair": 0}
+                  }
+_ATTN_ENV = ("bwd_fused",)
 _attn_opts = dict(_ATTN_DEFAULTS)
 
 
 def _attn_env() -> dict:
     env = {}
-    for key, conv in (("fwd_pipe", int), ("fwd_thr", float), ("dkdv_impl", int), ("dq_pipe", int),
-                      ("dkdv_split", int), ("dkdv_kreg", int), ("bwd_fused", int),
-                      ("bwd_window", int), ("fwd_order", int), ("dq_order", int), ("dkdv_order", int),
-                      ("wave_pair", int)):
+    for key in _ATTN_ENV:
         name = "PYRECOVER_ATTN_" + key.upper()
         v = os.environ.get(name)
         if v is not None and v != "":
             try:
-                env[key] = conv(v)
+                env[key] = int(v)
             except ValueError:
-                raise ValueError(f"{name}={v!r} is not a valid {conv.__name__}") from None
+                raise ValueError(f"{name}={v!r} is not a valid int") from None
     return env
 
 
@@ -96,15 +96,15 @@ def _apply_options(mod, env: dict) -> None:
     opts.update(env)
     mod.attn_set_options(opts["fwd_pipe"], opts["fwd_thr"], opts["dkdv_impl"], opts["dq_pipe"], opts["dkdv_split"],
                          opts["dkdv_kreg"], opts["bwd_fused"], opts["bwd_window"])
-    mod.attn_set_order(opts["fwd_order"], opts["dq_order"], opts["dkdv_order"], opts["wave_pair"])
+    mod.attn_set_order(opts["fwd_order"], opts["dq_order"], opts["dkdv_order"])
     _attn_opts.update(opts)
 
 
 def set_attn_options(**kw) -> dict:
     """Set attention kernel selection knobs (fwd_pipe, fwd_thr, dkdv_impl, dq_pipe, dkdv_split, dkdv_kreg,
-    bwd_fused, bwd_window, fwd_order, dq_order, dkdv_order, wave_pair); keys left out
+    bwd_fused, bwd_window, fwd_order, dq_order, dkdv_order); keys left out
     keep their value, ``None`` restores the default. Returns the previous settings."""
-    mod = native()  # loads the extension and applies the PYRECOVER_ATTN_* values first
+    mod = native()  # loads the extension and applies PYRECOVER_ATTN_BWD_FUSED first
     prev = dict(_attn_opts)
     new = {}
     for k, v in kw.items():

@@ -79,18 +79,19 @@ def _mm_into(slot, a, b, shape):
     slot.mm_(a, b, shape)
 
 
-# Weight gradients dW = dY^T X with K = tokens. hipBLASLt runs this GEMM ~25-30% faster when both
-# operands are K-contiguous ("TN": dYt [out, T] times Xt [in, T]^T) than on the row-major
-# activations, which is worth two bandwidth-bound HIP transposes for the large projections
-# (QKV, output projection, W1|W3, W2, output head; tools/gemm_bench.py --layouts).
-# PYRECOVER_TN_WGRAD=0 disables it.
-# SwiGLU backward kernel (csrc/kernels/elementwise.hip pra_swiglu_bwd): -1 = default (hoisted tile
-# kernel), 0 = grid-stride kernel (A/B: tools/step_ab.py)
-SWIGLU_BWD_VARIANT = int(os.environ.get("PYRECOVER_SWIGLU_BWD", "-1"))
-# inverse RoPE of dq / dk in the attention backward's epilogue (else a separate pass over dq|dk)
-FUSED_ROPE_BWD = os.environ.get("PYRECOVER_FUSED_ROPE_BWD", "1") == "1"
-TN_WGRAD = os.environ.get("PYRECOVER_TN_WGRAD", "1") == "1"
-TN_WGRAD_WO = TN_WGRAD and os.environ.get("PYRECOVER_TN_WGRAD_WO", "1") == "1"
+# Measured defaults, switchable only from code (tools/step_ab.py arms, tests; no environment knob):
+# * TN_WGRAD / TN_WGRAD_WO: library weight gradients dW = dY^T X (K = tokens) run on K-contiguous
+#   transposed copies ("TN": dYt [out, T] times Xt [in, T]^T), ~25-30% faster than on the row-major
+#   activations, which is worth two bandwidth-bound HIP transposes for the large projections (QKV,
+#   output projection, W1|W3, W2, output head; tools/gemm_bench.py --layouts);
+# * SWIGLU_BWD_VARIANT: SwiGLU backward kernel (csrc/kernels/elementwise.hip pra_swiglu_bwd), -1 =
+#   hoisted tile kernel, 0 = grid-stride kernel;
+# * FUSED_ROPE_BWD: inverse RoPE of dq / dk in the attention backward's epilogue (else a separate
+#   pass over dq|dk).
+SWIGLU_BWD_VARIANT = -1
+FUSED_ROPE_BWD = True
+TN_WGRAD = True
+TN_WGRAD_WO = True
 
 
 # Shape limits of the HIP kernels (outside them the op runs the torch math of ops/reference.py on

@@ -28,8 +28,8 @@ from ..parallel.flat import FlatParams
 
 # Matrices with a transposed weight shadow (parallel/flat.py) are updated by a tiled AdamW kernel
 # that writes the shadow from the values it just computed (no transpose pass re-reading the
-# weights); PRA_FUSED_ADAMW_T=0 falls back to flat AdamW + a separate transpose.
-FUSED_T = os.environ.get("PRA_FUSED_ADAMW_T", "1") == "1"
+# weights); False (from code: tests, A/B tools) falls back to flat AdamW + a separate transpose.
+FUSED_T = True
 # When an overlapped bucket update is enqueued on the side stream (PYRECOVER_OPT_SCHED):
 #   "attn" (default): held until the next attention backward, then enqueued behind an event recorded
 #            between its dQ and dK/dV kernels (ops.sched.attention_window), so it runs beside dK/dV,

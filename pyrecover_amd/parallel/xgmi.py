@@ -13,9 +13,9 @@ instead. Default engine (``csrc/dist/xgmi.cpp`` XgmiEngine, native):
   backward thread only records an event and enqueues the bucket (no Python in the critical window,
   one hardware queue for all of it).
 
-Per bucket, the traffic per link is bucket/W per phase. ``PYRECOVER_XGMI_ENGINE=copy`` selects the
-earlier copy-engine path (one copy stream per peer into local staging, then the reduction kernel,
-orchestrated by a Python thread).
+Per bucket, the traffic per link is bucket/W per phase. (Round 4's copy-engine path -- one copy
+stream per peer into local staging, then the reduction kernel, orchestrated by a Python thread -- was
+replaced by this engine and removed in round 6.)
 
 Cross-process ordering uses interprocess HIP events only: a rank's comm stream waits, on the GPU,
 on its peers' "bucket ready" / "slice reduced" events, and no kernel spins. The host only
@@ -30,8 +30,6 @@ xgmi``, ``bench.py --allreduce xgmi``. RCCL stays the default.
 from __future__ import annotations
 
 import os
-import queue
-import threading
 import time
 import uuid
 from multiprocessing import shared_memory
@@ -63,23 +61,16 @@ def _hidden_ranks(vis) -> List[int]:
     return sorted({r for r, (own, _) in enumerate(vis) for _, seen in vis if own not in seen})
 
 class _Work:
-    __slots__ = ("owner", "b", "ready", "seq")
+    __slots__ = ("owner", "b", "seq")
 
     def __init__(self, owner, b):
         self.owner = owner
         self.b = b
-        self.ready = threading.Event()
-        self.seq = 0  # native engine: the step this bucket belongs to (a ticket for wait)
+        self.seq = 0  # the step this bucket belongs to (a ticket for wait)
 
     def wait(self):
         """Current stream waits (GPU-side) for the all-reduced bucket."""
-        if self.owner.eng is not None:
-            self.owner.eng.wait(self.b, self.seq, torch.cuda.current_stream(self.owner.dev).cuda_stream)
-            return
-        self.ready.wait()
-        if self.owner.error is not None:
-            raise RuntimeError(f"xgmi all-reduce failed: {self.owner.error}")
-        torch.cuda.current_stream(self.owner.dev).wait_event(self.owner.ev_done[self.b])
+        self.owner.eng.wait(self.b, self.seq, torch.cuda.current_stream(self.owner.dev).cuda_stream)
 
 
 class _HostSeq:
@@ -116,6 +107,7 @@ class _HostSeq:
         self.a[self.rank, slot] = seq
 
     def wait(self, r: int, slot: int, seq: int, timeout: float = 600.0):
+        """Poll rank r's word until it reaches seq (the host side of the engine's wait_word)."""
         if self.a[r, slot] >= seq:
             return
         t0 = time.perf_counter()
@@ -123,7 +115,7 @@ class _HostSeq:
         while self.a[r, slot] < seq:
             spins += 1
             if spins > 200:
-                time.sleep(20e-6)  # releases the GIL for the backward thread
+                time.sleep(20e-6)
             if time.perf_counter() - t0 > timeout:
                 raise TimeoutError(f"xgmi: rank {r} did not publish slot {slot} seq {seq}")
 
@@ -230,115 +222,26 @@ class XgmiAllReduce:
         self.nb = nb
         self.seq = 1  # current step's sequence number (published values start at 1)
         self.hseq = _HostSeq(self.rank, W, 2 * nb + 1, self.hgroup)
-        self.error = None
-        self.eng = None
-        if os.environ.get("PYRECOVER_XGMI_ENGINE", "pull") != "copy":
-            # default: the native engine (csrc/dist/xgmi.cpp XgmiEngine) -- one comm stream, one
-            # pull-reduce kernel reading every peer's slice over xGMI and one pull-gather kernel per
-            # bucket, scheduled by a C++ worker thread
-            code = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}[self.dtype]
-            cuts = [c for sl in self.slices for c in [s0 for s0, _ in sl] + [sl[-1][1]]]
-            self.eng = self.C.XgmiEngine(
-                di, self.rank, W, code, self.esz, list(self.peer_base), cuts, self.hseq.address(),
-                list(self.ev_ready), list(self.ev_rs), self.ev_step,
-                [e for r in range(W) for e in self.peer_ready[r]], [e for r in range(W) for e in self.peer_rs[r]],
-                list(self.peer_step))
-        else:
-            # copy-engine path: per-peer copy streams into local staging, the rank-ordered reduction
-            # on a comm stream, orchestrated by a Python thread
-            max_slice = max((s1 - s0) for sl in self.slices for s0, s1 in sl)
-            self.stride = ((max_slice + 63) // 64) * 64
-            self.staging = torch.empty(max(1, (W - 1) * self.stride), dtype=self.dtype, device=self.dev)
-            self.ev_done = [torch.cuda.Event() for _ in range(nb)]
-            self.ev_sum = torch.cuda.Event()
-            self.comm = torch.cuda.Stream(device=self.dev)
-            self.copy = {r: torch.cuda.Stream(device=self.dev) for r in range(W) if r != self.rank}
-            self.q: "queue.Queue" = queue.Queue()
-            self.works: List[_Work] = []
-            self.th = threading.Thread(target=self._loop, name="pyrecover-xgmi", daemon=True)
-            self.th.start()
+        # the native engine (csrc/dist/xgmi.cpp XgmiEngine): one comm stream, one pull-reduce kernel
+        # reading every peer's slice over xGMI and one pull-gather kernel per bucket, scheduled by a
+        # C++ worker thread
+        code = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}[self.dtype]
+        cuts = [c for sl in self.slices for c in [s0 for s0, _ in sl] + [sl[-1][1]]]
+        self.eng = self.C.XgmiEngine(
+            di, self.rank, W, code, self.esz, list(self.peer_base), cuts, self.hseq.address(),
+            list(self.ev_ready), list(self.ev_rs), self.ev_step,
+            [e for r in range(W) for e in self.peer_ready[r]], [e for r in range(W) for e in self.peer_rs[r]],
+            list(self.peer_step))
         dist.barrier(group=self.hgroup)
 
     # --- backward thread -----------------------------------------------------------------
     def launch(self, b: int) -> _Work:
         w = _Work(self, b)
-        if self.eng is not None:
-            w.seq = self.eng.launch(b, torch.cuda.current_stream(self.dev).cuda_stream)
-            return w
-        self.C.event_record(self.ev_ready[b], torch.cuda.current_stream(self.dev).cuda_stream)
-        self.q.put((b, w))
+        w.seq = self.eng.launch(b, torch.cuda.current_stream(self.dev).cuda_stream)
         return w
 
     def end_step(self):
         """After every bucket of the step was waited on: no rank may overwrite its gradient
         buffer (next backward) before every peer finished reading it."""
-        if self.eng is not None:
-            self.eng.end_step(torch.cuda.current_stream(self.dev).cuda_stream)
-            self.seq += 1
-            return
-        done = threading.Event()
-        self.q.put(("step", done))
-        done.wait()
-        if self.error is not None:
-            raise RuntimeError(f"xgmi all-reduce failed: {self.error}")
-        cur = torch.cuda.current_stream(self.dev).cuda_stream
-        for r in range(self.world):
-            if r != self.rank:
-                self.C.stream_wait_event(cur, self.peer_step[r])
-
-    # --- comm thread ---------------------------------------------------------------------
-    def _loop(self):
-        torch.cuda.set_device(self.dev)
-        while True:
-            b, w = self.q.get()
-            try:
-                if b == "step":
-                    self.C.event_record(self.ev_step, self.comm.cuda_stream)
-                    self.hseq.publish(2 * self.nb, self.seq)
-                    for r in range(self.world):
-                        if r != self.rank:
-                            self.hseq.wait(r, 2 * self.nb, self.seq)
-                    self.seq += 1
-                else:
-                    self._bucket(b)
-            except Exception as e:  # surfaced by the waiter
-                self.error = repr(e)
-            w.set() if b == "step" else w.ready.set()
-
-    def _stage(self, r):
-        k = r if r < self.rank else r - 1
-        return self.staging.data_ptr() + k * self.stride * self.esz
-
-    def _bucket(self, b):
-        C, me, es = self.C, self.rank, self.esz
-        sl = self.slices[b]
-        s0, s1 = sl[me]
-        n = s1 - s0
-        hs, seq = self.hseq, self.seq
-        hs.publish(b, seq)  # ev_ready[b] was recorded (launch) before this bucket was queued
-        # reduce-scatter: pull my slice from every peer, all links at once
-        for r, cs in self.copy.items():
-            h = cs.cuda_stream
-            hs.wait(r, b, seq)  # peer r recorded its ev_ready[b] of this step
-            C.stream_wait_event(h, self.peer_ready[r][b])
-            cs.wait_event(self.ev_sum)  # staging reused: previous bucket's reduction consumed it
-            C.copy_async(self._stage(r), self.peer_base[r] + s0 * es, n * es, h)
-        comm = self.comm
-        C.stream_wait_event(comm.cuda_stream, self.ev_ready[b])
-        for cs in self.copy.values():
-            comm.wait_stream(cs)
-        srcs = [(self.peer_base[me] + s0 * es) if r == me else self._stage(r) for r in range(self.world)]
-        C.sum_slices(srcs, self.peer_base[me] + s0 * es, n, self.dtype, comm.cuda_stream)
-        self.ev_sum.record(comm)
-        C.event_record(self.ev_rs[b], comm.cuda_stream)
-        hs.publish(self.nb + b, seq)
-        # all-gather: pull each owner's reduced slice into my buffer
-        for r, cs in self.copy.items():
-            h = cs.cuda_stream
-            hs.wait(r, self.nb + b, seq)  # peer r recorded its ev_rs[b] of this step
-            C.stream_wait_event(h, self.peer_rs[r][b])
-            p0, p1 = sl[r]
-            C.copy_async(self.peer_base[me] + p0 * es, self.peer_base[r] + p0 * es, (p1 - p0) * es, h)
-        for cs in self.copy.values():
-            comm.wait_stream(cs)
-        self.ev_done[b].record(comm)
+        self.eng.end_step(torch.cuda.current_stream(self.dev).cuda_stream)
+        self.seq += 1

@@ -33,5 +33,4 @@ def attn_opts(cuda):
 
     yield _ext.set_attn_options
     _ext.set_attn_options(fwd_pipe=None, fwd_thr=None, dkdv_impl=None, dq_pipe=None, dkdv_split=None, dkdv_kreg=None,
-                          bwd_fused=None, bwd_window=None, fwd_order=None, dq_order=None, dkdv_order=None,
-                          wave_pair=None)
+                          bwd_fused=None, bwd_window=None, fwd_order=None, dq_order=None, dkdv_order=None)

@@ -220,10 +220,9 @@ def _qkv(cuda, B, S, Hq, Hkv, D, seed=0, scale=1.0):
 @pytest.mark.parametrize("B,S,Hq,Hkv,D", [(1, 256, 4, 4, 128), (2, 512, 8, 2, 128), (1, 384, 4, 1, 64),
                                           (1, 128, 2, 2, 64), (1, 192, 4, 2, 128)])
 @pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("pipe", [0, 1, 2])
+@pytest.mark.parametrize("pipe", [0, 1])
 def test_attention_fwd(cuda, attn_opts, pipe, B, S, Hq, Hkv, D, causal):
-    """Every forward kernel (fwd_pipe: fwd_kernel / cross-tile pipelined fwd_p_kernel / 16x16x32
-    fwd16_kernel for causal head_dim 128, the pipelined kernel otherwise)."""
+    """Every forward kernel (fwd_pipe: fwd_kernel / cross-tile pipelined fwd_p_kernel)."""
     attn_opts(fwd_pipe=pipe)
     C = _ext.native()
     _, q, k, v = _qkv(cuda, B, S, Hq, Hkv, D)
@@ -238,33 +237,33 @@ def test_attention_fwd(cuda, attn_opts, pipe, B, S, Hq, Hkv, D, causal):
                                                  (2, 768, 16, 4, 64, False)])
 @pytest.mark.parametrize("kreg", [-2, 0])
 def test_attention_block_order_is_bitwise_neutral(cuda, attn_opts, kreg, B, S, Hq, Hkv, D, causal):
-    """The XCD-grouped block order (fwd_order / dq_order / dkdv_order) and the wave pairing only change
-    which workgroup / wave computes which tile: every setting gives the same bits as the heavy-first
-    order, forward and backward (ring and LDS dK/dV kernels), and matches the fp32 oracle."""
+    """The XCD-grouped block order (fwd_order / dq_order / dkdv_order) only changes which workgroup
+    computes which tile: every setting gives the same bits as the heavy-first order, forward and
+    backward (ring and LDS dK/dV kernels), and matches the fp32 oracle."""
     C = _ext.native()
     _, q, k, v = _qkv(cuda, B, S, Hq, Hkv, D, seed=7)
     do = torch.randn(B, S, Hq, D, device=cuda).bfloat16()
     scale = 1 / math.sqrt(D)
     outs = {}
-    cases = [(0, 0), (1, 0), (2, 0), (4, 0), (-1, 0), (0, 1), (-1, 1)]
-    for order, pair in cases:
-        attn_opts(fwd_order=order, dq_order=order, dkdv_order=order, dkdv_kreg=kreg, wave_pair=pair)
+    cases = [0, 1, 2, 4, -1]
+    for order in cases:
+        attn_opts(fwd_order=order, dq_order=order, dkdv_order=order, dkdv_kreg=kreg)
         o, lse = C.attn_fwd(q, k, v, scale, causal)
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         C.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, causal)
-        outs[order, pair] = (o, lse, dq, dk, dv)
+        outs[order] = (o, lse, dq, dk, dv)
     for case in cases[1:]:
-        assert all(torch.equal(a, b) for a, b in zip(outs[0, 0], outs[case])), case
+        assert all(torch.equal(a, b) for a, b in zip(outs[0], outs[case])), case
     qf, kf, vf = (t.float().requires_grad_() for t in (q, k, v))
     of, _ = R.attention_lse_ref(qf, kf, vf, causal, scale)
     of.backward(do.float())
-    o, _, dq, dk, dv = outs[-1, 1]
+    o, _, dq, dk, dv = outs[-1]
     assert (o.float() - of).abs().max().item() < 2e-2
     for got, want in ((dq, qf.grad), (dk, kf.grad), (dv, vf.grad)):
         assert _rel(got, want) < 3e-2, (_rel(got, want))
 
 
-@pytest.mark.parametrize("pipe", [0, 1, 2])
+@pytest.mark.parametrize("pipe", [0, 1])
 @pytest.mark.parametrize("thr", [0.0, 8.0])
 def test_attention_fwd_rescale_spike(cuda, attn_opts, pipe, thr):
     """Forces the online-softmax running max to jump at a late key tile (rule 26), with the exact
@@ -684,38 +683,3 @@ def test_wgrad_mm_split_tail_under_hip_graph_capture(cuda):
     assert ((out.float() - exact).norm() / exact.norm()).item() < 5e-3
 
 
-@pytest.fixture
-def wgrad_streamk():
-    C_ = _ext.native()
-    prev = C_.wgrad_get_streamk()
-    yield C_.wgrad_set_streamk
-    C_.wgrad_set_streamk(prev)
-
-
-@pytest.mark.parametrize("K,M,N", [(2048, 6144, 4096), (1024, 7680, 2560), (96, 1280, 256), (64, 256, 256),
-                                   (4096, 4096, 14336)])
-@pytest.mark.parametrize("accumulate", [False, True])
-def test_wgrad_mm_streamk_vs_fp32(cuda, wgrad_streamk, K, M, N, accumulate):
-    """The stream-K schedule (one workgroup per CU, each an equal share of the tile x k-step
-    iterations; tiles covered by several workgroups summed from fp32 partials in k order by the last
-    arriver): against an fp64 oracle, with accumulate, bit-identical run to run -- including ranges
-    shorter than one tile (few tiles, short K) -- and within rounding of the default schedule."""
-    C_ = _ext.native()
-    g = torch.Generator(device=cuda)
-    g.manual_seed(K + M + N)
-    a = torch.randn(K, M, device=cuda, generator=g).bfloat16()
-    b = torch.randn(K, N, device=cuda, generator=g).bfloat16()
-    c0 = torch.randn(M, N, device=cuda, generator=g).bfloat16()
-    wgrad_streamk(2)
-    out = c0.clone()
-    C_.wgrad_mm_(a, b, out, accumulate)
-    ref = a.double().t() @ b.double() + (c0.double() if accumulate else 0)
-    err = ((out.double() - ref).abs() / (ref.abs() + math.sqrt(K))).max().item()
-    assert err < 1e-2, err
-    out2 = c0.clone()
-    C_.wgrad_mm_(a, b, out2, accumulate)
-    assert torch.equal(out, out2)  # deterministic
-    wgrad_streamk(0)
-    out3 = c0.clone()
-    C_.wgrad_mm_(a, b, out3, accumulate)
-    assert ((out3.float() - out.float()).abs() <= out.float().abs() * 2 ** -7 + 1e-2).all().item()

@@ -1,7 +1,6 @@
 """Direct xGMI all-reduce backend (pyrecover_amd/parallel/xgmi.py) with 2 ranks sharing one GPU:
 IPC memory + IPC events across processes; the native pull engine (one pull-reduce and one
-pull-gather kernel per bucket on one stream, C++ worker: the default) and the copy-engine path
-(per-peer copy streams, rank-ordered reduction, PYRECOVER_XGMI_ENGINE=copy).
+pull-gather kernel per bucket on one stream, C++ worker).
 Checks the all-reduce result against the fp32 sum and that 3 training steps with backend="xgmi"
 equal the same steps with the default process-group all-reduce (bit-exact: for 2 ranks the fp32
 sum rounded once equals the bf16 sum). Multi-GPU bandwidth is not measured here."""
@@ -17,10 +16,9 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(tmp_path, backend, port, overlap=False, engine="pull"):
-    out = tmp_path / f"{backend}{'_ov' if overlap else ''}_{engine}.pt"
-    env = dict(os.environ, PYRECOVER_LOCAL_DEVICE="0", PYRECOVER_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0",
-               PYRECOVER_XGMI_ENGINE=engine)
+def _run(tmp_path, backend, port, overlap=False):
+    out = tmp_path / f"{backend}{'_ov' if overlap else ''}.pt"
+    env = dict(os.environ, PYRECOVER_LOCAL_DEVICE="0", PYRECOVER_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "tests", "dist_workers", "xgmi_worker.py"),
            "--backend", backend, "--out", str(out)] + (["--overlap"] if overlap else [])
@@ -29,14 +27,13 @@ def _run(tmp_path, backend, port, overlap=False, engine="pull"):
     return torch.load(out, weights_only=True)
 
 
-@pytest.mark.parametrize("engine", ["pull", "copy"])
-def test_xgmi_allreduce_matches_process_group(cuda, tmp_path, engine):
-    port = 29531 if engine == "pull" else 29551
+def test_xgmi_allreduce_matches_process_group(cuda, tmp_path):
+    port = 29531
     a = _run(tmp_path, "rccl", port)
-    b = _run(tmp_path, "xgmi", port + 1, engine=engine)
+    b = _run(tmp_path, "xgmi", port + 1)
     assert b["direct_err"] == 0.0 and a["direct_err"] == 0.0
     assert torch.equal(a["params"], b["params"])
-    c = _run(tmp_path, "xgmi", port + 2, overlap=True, engine=engine)
+    c = _run(tmp_path, "xgmi", port + 2, overlap=True)
     assert torch.equal(a["params"], c["params"])
 
 

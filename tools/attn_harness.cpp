@@ -72,17 +72,16 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&dk, (size_t)B * S * Hkv * D * 2));
   CK(hipMalloc(&dv, (size_t)B * S * Hkv * D * 2));
   CK(hipMalloc(&lse, (size_t)B * Hq * S * 4));
-  // PRA_BWD_FUSED=0/1: split dQ + dK/dV kernels or the fused backward; PRA_FWD_PIPE=0/1/2: forward
-  // kernel (fwd_kernel / pipelined fwd_p_kernel / 16x16x32 fwd16_kernel); unset = the defaults
+  // PRA_BWD_FUSED=0/1: split dQ + dK/dV kernels or the fused backward; PRA_FWD_PIPE=0/1: forward
+  // kernel (fwd_kernel / pipelined fwd_p_kernel); unset = the defaults
   {
     const char* f = getenv("PRA_FWD_PIPE");
     const char* e = getenv("PRA_BWD_FUSED");
     if (f || e) pra_attn_set_options(f ? atoi(f) : -1, 8.f, -1, -1, 1, -2, e ? atoi(e) : 0, 0);
-    // PRA_ATTN_ORDER="f,q,k[,pair]": block order of the forward / dQ / dK/dV grids and the wave pairing
-    // (pra_attn_set_order)
-    int of = 0, oq = 0, ok = 0, op = 0;
-    if (const char* o = getenv("PRA_ATTN_ORDER")) sscanf(o, "%d,%d,%d,%d", &of, &oq, &ok, &op);
-    pra_attn_set_order(of, oq, ok, op);
+    // PRA_ATTN_ORDER="f,q,k": block order of the forward / dQ / dK/dV grids (pra_attn_set_order)
+    int of = 0, oq = 0, ok = 0;
+    if (const char* o = getenv("PRA_ATTN_ORDER")) sscanf(o, "%d,%d,%d", &of, &oq, &ok);
+    pra_attn_set_order(of, oq, ok);
   }
   const long nws = pra_attn_bwd_workspace(pra::kBF16, B, S, Hq, Hkv, D);
   CK(hipMalloc(&ws, (size_t)nws * 4));

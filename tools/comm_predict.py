@@ -172,12 +172,15 @@ def main():
         rows = torch.randn(n_tok, cfg.dim, device=dev).bfloat16()
         ids = torch.randint(0, cfg.vocab_size, (n_tok,), device=dev)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        ev[0].record()
-        for _ in range(a.world):
-            emb.index_add_(0, ids, rows.float())
-        torch.sort(ids)
-        ev[1].record()
-        torch.cuda.synchronize()
+        for rep in range(3):  # the first pass loads the kernels
+            ev[0].record()
+            torch.sort(ids)
+            sel = emb.index_select(0, ids)
+            for _ in range(a.world):
+                emb.index_add_(0, ids, rows.float())
+            emb.index_copy_(0, ids, sel)
+            ev[1].record()
+            torch.cuda.synchronize()
         sparse_extra = ev[0].elapsed_time(ev[1])
     nb = timer.nb
     ready = [0.0] * nb

@@ -26,8 +26,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def parse_arm(spec):
     """`opt.ATTR=value` sets an attribute of the optimizer instance; `attn.OPTION=value` an
-    attention kernel option (_ext.set_attn_options); `wgrad.streamk=N` the weight-gradient GEMM's
-    schedule (C.wgrad_set_streamk); the item `noupdate` skips the AdamW update
+    attention kernel option (_ext.set_attn_options); the item `noupdate` skips the AdamW update
     kernels (a diagnostic arm: what the optimizer costs the step)."""
     name, _, body = spec.partition(":")
     sets = []
@@ -37,7 +36,7 @@ def parse_arm(spec):
             continue
         lhs, _, rhs = item.partition("=")
         mod, _, attr = lhs.strip().rpartition(".")
-        if mod in ("attn", "wgrad"):  # attention option / wgrad.streamk (C.wgrad_set_streamk)
+        if mod == "attn":  # attention option
             sets.append((mod, attr, ast.literal_eval(rhs.strip())))
             continue
         target = "opt" if mod == "opt" else importlib.import_module("pyrecover_amd." + mod)
@@ -95,7 +94,7 @@ def main():
     def resolve(sets):
         out = []
         for m, k, v in sets:
-            if m in ("attn", "wgrad"):
+            if m == "attn":
                 continue
             m = opt if m == "opt" else m
             if v == "noupdate":
@@ -106,10 +105,6 @@ def main():
     def run(arm, n):
         attn = {k: v for m, k, v in arm[1] if m == "attn"}
         prev_attn = _ext.set_attn_options(**attn) if attn else None
-        sk = [v for m, k, v in arm[1] if m == "wgrad" and k == "streamk"]
-        prev_sk = _ext.native().wgrad_get_streamk()
-        if sk:
-            _ext.native().wgrad_set_streamk(int(sk[-1]))
         sets = resolve(arm[1])
         old = [(m, k, m.__dict__[k] if k in m.__dict__ else getattr(m, k)) for m, k, _ in sets]
         for m, k, v in sets:
@@ -122,7 +117,6 @@ def main():
             torch.cuda.synchronize()
             return (time.perf_counter() - t0) * 1000 / n, float(loss.item())
         finally:
-            _ext.native().wgrad_set_streamk(prev_sk)
             if prev_attn is not None:
                 _ext.set_attn_options(**prev_attn)
             for m, k, v in old:

@@ -4,7 +4,6 @@ kernel (csrc/kernels/gemm_wgrad.hip, C.wgrad_mm_) against hipBLASLt in the layou
   tn      torch.mm(dYt, Xt.t()) on pre-transposed copies (the library's fast layout, copies free)
   tn+T    the two HIP transposes + tn                 (what the default step pays)
   hip     C.wgrad_mm_(dY, X, out)
-  hip_sk  the same kernel with the stream-K schedule (C.wgrad_set_streamk(2))
 Checks hip against an fp32 reference first. Rounds interleaved in one process (rule: A/B in one
 process); prints one JSON line per shape with median us and TFLOP/s.
 
@@ -58,20 +57,6 @@ def main():
         err2 = (out2.float() - (ref + c0.float())).abs().max().item() / ref.abs().max().item()
         print(json.dumps({"check": name, "rel_err": err, "rel_err_acc": err2}), flush=True)
         assert err < 1e-2 and err2 < 1e-2, (name, err, err2)
-    sk0 = C.wgrad_get_streamk()
-    # stream-K schedule (C.wgrad_set_streamk(2)) against the same fp32 reference
-    for name, M, N in SHAPES:
-        K = 1024
-        dy = torch.randn(K, M, device=dev).bfloat16()
-        x = torch.randn(K, N, device=dev).bfloat16()
-        ref = dy.float().t() @ x.float()
-        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-        C.wgrad_set_streamk(2)
-        C.wgrad_mm_(dy, x, out, False)
-        C.wgrad_set_streamk(sk0)
-        err = (out.float() - ref).abs().max().item() / ref.abs().max().item()
-        print(json.dumps({"check_streamk": name, "rel_err": err}), flush=True)
-        assert err < 1e-2, (name, err)
     T = args.tokens
     sel = set(args.shapes.split(",")) if args.shapes else None
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -88,7 +73,6 @@ def main():
             "tn": lambda: torch.mm(dyT, xT.t(), out=out),
             "tn+T": lambda: torch.mm(C.transpose2d(dy, dyT), C.transpose2d(x, xT).t(), out=out),
             "hip": lambda: C.wgrad_mm_(dy, x, out, False),
-            "hip_sk": lambda: (C.wgrad_set_streamk(2), C.wgrad_mm_(dy, x, out, False), C.wgrad_set_streamk(sk0)),
         }
         res = {k: [] for k in arms}
         for _ in range(args.rounds):
