@@ -26,7 +26,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def parse_arm(spec):
     """`opt.ATTR=value` sets an attribute of the optimizer instance; `attn.OPTION=value` an
-    attention kernel option (_ext.set_attn_options); the item `noupdate` skips the AdamW update
+    attention kernel option (_ext.set_attn_options); `native.SETTER=value` calls that setter of the
+    extension before the arm's steps and with 0 after them; the item `noupdate` skips the AdamW update
     kernels (a diagnostic arm: what the optimizer costs the step)."""
     name, _, body = spec.partition(":")
     sets = []
@@ -36,7 +37,7 @@ def parse_arm(spec):
             continue
         lhs, _, rhs = item.partition("=")
         mod, _, attr = lhs.strip().rpartition(".")
-        if mod == "attn":  # attention option
+        if mod in ("attn", "native"):  # attention option / native setter C.<attr>(value), reset to 0 after
             sets.append((mod, attr, ast.literal_eval(rhs.strip())))
             continue
         target = "opt" if mod == "opt" else importlib.import_module("pyrecover_amd." + mod)
@@ -94,7 +95,7 @@ def main():
     def resolve(sets):
         out = []
         for m, k, v in sets:
-            if m == "attn":
+            if m in ("attn", "native"):
                 continue
             m = opt if m == "opt" else m
             if v == "noupdate":
@@ -105,6 +106,9 @@ def main():
     def run(arm, n):
         attn = {k: v for m, k, v in arm[1] if m == "attn"}
         prev_attn = _ext.set_attn_options(**attn) if attn else None
+        natives = [(k, v) for m, k, v in arm[1] if m == "native"]
+        for k, v in natives:
+            getattr(_ext.native(), k)(v)
         sets = resolve(arm[1])
         old = [(m, k, m.__dict__[k] if k in m.__dict__ else getattr(m, k)) for m, k, _ in sets]
         for m, k, v in sets:
@@ -117,6 +121,8 @@ def main():
             torch.cuda.synchronize()
             return (time.perf_counter() - t0) * 1000 / n, float(loss.item())
         finally:
+            for k, _ in natives:
+                getattr(_ext.native(), k)(0)
             if prev_attn is not None:
                 _ext.set_attn_options(**prev_attn)
             for m, k, v in old:
