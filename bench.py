@@ -322,7 +322,7 @@ def main():
                        "optimizer": "AdamW (flat fused HIP)" + ("" if args.no_overlap_optimizer else
                                                                  f", overlapped with backward ({_opt_sched(B * S)})"),
                        "adamw_math": "hw rcp/sqrt (fast)" if _adamw_fast() else "torch _fused_adamw_ bit-exact",
-                       "weight_shadows": bool(getattr(flat, "t_mats", None)),
+                       "weight_shadows": ",".join(getattr(flat, "shadow_sites", ())) or False,
                        "hand_written_gemms": _gemm_sites(B * S, cfg.dim)},
             "tokens_per_sec_per_gpu": round(tps / world, 2),
             "model_tflops_per_gpu": round(fpt * tps / world / 1e12, 2),

@@ -197,35 +197,58 @@ class Transformer(nn.Module):
         g.append([("output.weight", self.output.weight)])
         return g
 
-    def flatten_(self, tokens_per_step: Optional[int] = None, shadows: Optional[bool] = None) -> FlatParams:
+    SHADOW_SITES = ("qkv", "o", "w13", "w2", "head")
+
+    def flatten_(self, tokens_per_step: Optional[int] = None, shadows=None) -> FlatParams:
         """Move all parameters/gradients into flat buffers (call after the final .to(device/dtype)).
 
         Transposed weight shadows (K-contiguous W^T for the data-gradient GEMMs, rewritten by the
-        optimizer): +3.5% at 7B B16 (profiles/ab_weight_shadows_s7.log), +5% at 7B B1 (99.1 vs
-        104.1-104.4 ms), -0.5% at Llama-3-8B B1 (108.1 vs 107.6 ms; profiles/r4/shadow_policy_b1/),
-        so they are on at every batch size. PRA_WEIGHT_SHADOWS=0 (or ``shadows=False``: the sharded
-        optimizer, whose owned chunks cut matrices, would re-derive every shadow after the parameter
-        all-gather) turns them off; PRA_WEIGHT_SHADOWS_HEAD=0 leaves the output head without one."""
+        optimizer), measured with bench.py on MI355X (profiles/r6/shadows/): +3.5% at 7B B16, +7.6% at
+        7B B1, +1.3% at 7B B4, +2% at Llama-3-8B S8192 B1, but -1.5% at Llama-3-8B S2048 B1, where no
+        single site accounts for it (dropping any one of qkv / o / w13 / w2 / head moves the step by
+        -0.4..+0.4%; dropping all of them, the optimizer runs the plain flat update instead of the
+        transposing one). ``shadows`` (default: env PRA_WEIGHT_SHADOWS, "auto") is "auto" (every
+        site, except none for a grouped-query model at <= 4096 tokens per step), True / "1" (every
+        site), False / "0" (none: e.g. the sharded optimizer, whose owned chunks cut matrices and
+        would re-derive every shadow after the parameter all-gather) or a comma list of
+        SHADOW_SITES.
+        """
         if self.flat is None:
             self.flat = FlatParams(self.fusion_groups())
             # optimizer-state indices follow model.parameters() order, as in the reference
             self.flat.module_order = list(self.parameters())
             if shadows is None:
-                shadows = os.environ.get("PRA_WEIGHT_SHADOWS", "1") != "0"
-            head = os.environ.get("PRA_WEIGHT_SHADOWS_HEAD", "1") == "1"
-            for mats in self._gemm_weights(head) if shadows else []:
+                shadows = os.environ.get("PRA_WEIGHT_SHADOWS", "auto")
+            if str(shadows).strip().lower() == "auto":
+                gqa = self.model_args.kv_heads < self.model_args.n_heads
+                shadows = not (gqa and tokens_per_step is not None and tokens_per_step <= 4096)
+            self.flat.shadow_sites = self.shadow_sites(shadows)
+            for mats in self._gemm_weights(self.flat.shadow_sites):
                 self.flat.register_transposed(mats, (sum(p.shape[0] for p in mats), mats[0].shape[1]))
             # parameters written through the module API must refresh the transposed shadows
             self.register_load_state_dict_post_hook(lambda mod, keys: mod.flat.refresh_transposed())
         return self.flat
 
-    def _gemm_weights(self, head: bool = True) -> List[List[nn.Parameter]]:
+    @classmethod
+    def shadow_sites(cls, spec) -> Tuple[str, ...]:
+        if spec is True or str(spec).strip().lower() in ("1", "all", "true"):
+            return cls.SHADOW_SITES
+        if spec is False or str(spec).strip().lower() in ("0", "none", "false", ""):
+            return ()
+        sites = tuple(s.strip() for s in str(spec).split(",") if s.strip())
+        bad = [s for s in sites if s not in cls.SHADOW_SITES]
+        if bad:
+            raise ValueError(f"unknown weight-shadow sites {bad}; choose from {cls.SHADOW_SITES}")
+        return sites
+
+    def _gemm_weights(self, sites: Sequence[str] = SHADOW_SITES) -> List[List[nn.Parameter]]:
         out = []
         for layer in self.layers.values():
             at, ff = layer.attention, layer.feed_forward
-            out += [[at.wq.weight, at.wk.weight, at.wv.weight], [at.wo.weight], [ff.w1.weight, ff.w3.weight],
-                    [ff.w2.weight]]
-        if head:
+            per = {"qkv": [at.wq.weight, at.wk.weight, at.wv.weight], "o": [at.wo.weight],
+                   "w13": [ff.w1.weight, ff.w3.weight], "w2": [ff.w2.weight]}
+            out += [per[s] for s in ("qkv", "o", "w13", "w2") if s in sites]
+        if "head" in sites:
             out.append([self.output.weight])
         return out
 

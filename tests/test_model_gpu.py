@@ -259,10 +259,10 @@ def test_transposed_weight_shadows_track_parameters(cuda):
 
 
 def test_weight_shadows_off_gives_the_same_gradients(cuda, monkeypatch):
-    """PRA_WEIGHT_SHADOWS=0 (data-gradient GEMMs read W as stored) matches the shadowed path up to
-    GEMM rounding."""
+    """PRA_WEIGHT_SHADOWS=0 (data-gradient GEMMs read W as stored) and a site list (shadows at the
+    O and W2 GEMMs only) match the shadowed path up to GEMM rounding."""
     grads = []
-    for flag in ("1", "0"):
+    for flag in ("1", "0", "o,w2"):
         monkeypatch.setenv("PRA_WEIGHT_SHADOWS", flag)
         torch.manual_seed(0)
         a = get_preset("llama-tiny", seq_len=256)
@@ -272,7 +272,9 @@ def test_weight_shadows_off_gives_the_same_gradients(cuda, monkeypatch):
             m = Transformer(a)
         torch.set_default_dtype(prev)
         flat = m.flatten_()
-        assert (flat.weight_t(m._gemm_weights()[0]) is None) == (flag == "0")
+        qkv, o = m._gemm_weights()[:2]
+        assert (flat.weight_t(qkv) is None) == (flag != "1")
+        assert (flat.weight_t(o) is None) == (flag == "0")
         g = torch.Generator(device=cuda)
         g.manual_seed(7)
         t = torch.randint(0, a.vocab_size, (2, 257), device=cuda, generator=g)
@@ -280,8 +282,9 @@ def test_weight_shadows_off_gives_the_same_gradients(cuda, monkeypatch):
         m(t[:, :-1], labels=t[:, 1:]).backward()
         torch.cuda.synchronize()
         grads.append(flat.grad.float().clone())
-    rel = ((grads[0] - grads[1]).norm() / grads[0].norm()).item()
-    assert rel < 1e-2, rel
+    for other in grads[1:]:
+        rel = ((grads[0] - other).norm() / grads[0].norm()).item()
+        assert rel < 1e-2, rel
 
 
 @pytest.mark.parametrize("dtype", ["fp16", "fp32", "fp64", "bf16+master"])

@@ -116,3 +116,24 @@ def test_wgrad_auto_needs_one_tile_per_cu(monkeypatch):
     assert not fused._wgrad_fills_chip(t, (5632, 1024))  # GPT-2-medium W1|W3: 88 tiles
     assert fused._wgrad_fills_chip(t, (4096, 4096))  # 7B O: 256 tiles
     assert fused._wgrad_fills_chip(t, (22016, 4096))  # 7B W1|W3: 1376 tiles
+
+
+def test_weight_shadow_site_policy(monkeypatch):
+    """PRA_WEIGHT_SHADOWS: auto (none for a grouped-query model at <= 4096 tokens per step, every
+    site otherwise: profiles/r6/shadows/), 1 / 0 and site lists; unknown sites are refused."""
+    monkeypatch.delenv("PRA_WEIGHT_SHADOWS", raising=False)
+    assert Transformer.shadow_sites("1") == Transformer.SHADOW_SITES
+    assert Transformer.shadow_sites(False) == ()
+    assert Transformer.shadow_sites("o, w2") == ("o", "w2")
+    with pytest.raises(ValueError):
+        Transformer.shadow_sites("qkv,mlp")
+
+    def sites(tokens, **over):
+        return Transformer(get_preset("llama-tiny", seq_len=64, **over)).flatten_(tokens_per_step=tokens).shadow_sites
+
+    assert sites(2048, n_kv_heads=2) == ()  # GQA at 2048 tokens (Llama-3-8B S2048 B1)
+    assert sites(8192, n_kv_heads=2) == Transformer.SHADOW_SITES  # GQA at 8192 tokens
+    assert sites(2048, n_kv_heads=4) == Transformer.SHADOW_SITES  # MHA (Llama-2-7B B1)
+    monkeypatch.setenv("PRA_WEIGHT_SHADOWS", "w13,head")
+    flat = Transformer(get_preset("llama-tiny", seq_len=64, n_kv_heads=2)).flatten_(tokens_per_step=2048)
+    assert flat.shadow_sites == ("w13", "head")  # (shadows themselves exist only for 16-bit GPU buffers)
