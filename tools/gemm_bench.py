@@ -19,6 +19,9 @@ def main():
     ap.add_argument("--dim", type=int, default=4096)
     ap.add_argument("--ffn", type=int, default=11008)
     ap.add_argument("--vocab", type=int, default=32000)
+    ap.add_argument("--qkv-out", type=int, default=0, help="QKV output width (GQA); default 3 x dim")
+    ap.add_argument("--hip", action="store_true", help="also time the hand-written NT kernel (gemm_nt_) for "
+                                                       "the forward and the shadowed data gradient")
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--no-table", action="store_true")
     ap.add_argument("--layouts", action="store_true", help="also time K-contiguous wgrad / transpose variants")
@@ -39,7 +42,7 @@ def main():
         configure_gemm_tuning("off" if a.no_table else "auto")
     dev = torch.device("cuda", 0)
     T, Dm, F, V = a.tokens, a.dim, a.ffn, a.vocab
-    outs = {"qkv": 3 * Dm, "wo": Dm, "w13": 2 * F, "w2": Dm, "head": V}
+    outs = {"qkv": a.qkv_out or 3 * Dm, "wo": Dm, "w13": 2 * F, "w2": Dm, "head": V}
     ins = {"qkv": Dm, "wo": Dm, "w13": Dm, "w2": F, "head": Dm}
     res = {}
     for name in outs:
@@ -58,6 +61,14 @@ def main():
                           "dgrad_wT": lambda: torch.mm(dy, wT.t()),
                           "dgrad_TT": lambda: torch.mm(dyT.t(), wT.t()),
                           "transpose_dy": lambda: dy.t().contiguous(), "transpose_x": lambda: x.t().contiguous()})
+        if a.hip and n_out % 256 == 0 and n_in % 256 == 0 and T % 256 == 0:
+            from pyrecover_amd import _ext
+
+            C = _ext.native()
+            wT = w.t().contiguous()
+            y = torch.empty(T, n_out, dtype=x.dtype, device=dev)
+            dx = torch.empty(T, n_in, dtype=x.dtype, device=dev)
+            cases.update({"fwd_hip": lambda: C.gemm_nt_(x, w, y), "dgrad_hip": lambda: C.gemm_nt_(dy, wT, dx)})
         for cname, fn in cases.items():
             for _ in range(3):
                 fn()
