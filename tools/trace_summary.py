@@ -16,6 +16,8 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--by-grid", action="store_true", help="split GEMM kernels by grid size")
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--overlap", action="store_true",
+                    help="per kernel: mean duration of the calls that ran beside the AdamW update vs alone")
     a = ap.parse_args()
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
     starts = [i for i, r in enumerate(rows) if "embed_fwd_kernel" in r["Kernel_Name"]]
@@ -57,6 +59,47 @@ def main():
     print("ms_per_step,calls_per_step,kernel")
     for k, (ms, n) in sorted(per.items(), key=lambda x: -x[1][0])[:a.top]:
         print(f"{ms:.2f},{n // a.steps},{k}")
+    if a.overlap:
+        overlap_report(sel, a)
+
+
+def overlap_report(sel, a):
+    """Calls of each non-update kernel split by whether an AdamW kernel ran during most of them."""
+    upd = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in sel if "adamw" in r["Kernel_Name"])
+    merged = []
+    for s, e in upd:
+        if merged and s <= merged[-1][1]:
+            merged[-1][1] = max(merged[-1][1], e)
+        else:
+            merged.append([s, e])
+    import bisect
+
+    starts = [m[0] for m in merged]
+
+    def covered(s, e):
+        i = max(bisect.bisect_right(starts, s) - 1, 0)
+        c = 0
+        while i < len(merged) and merged[i][0] < e:
+            c += max(0, min(e, merged[i][1]) - max(s, merged[i][0]))
+            i += 1
+        return c
+
+    acc = collections.defaultdict(lambda: [0, 0.0, 0, 0.0])
+    for r in sel:
+        name = r["Kernel_Name"]
+        if "adamw" in name:
+            continue
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        key = ("GEMM grid " + r["Grid_Size_X"]) if "Cijk" in name else name[:70]
+        d = (e - s) / 1e3
+        k = 2 if e > s and covered(s, e) > 0.5 * (e - s) else 0
+        acc[key][k] += 1
+        acc[key][k + 1] += d
+    print("\nkernel, calls alone, mean us alone, calls beside the update, mean us beside, stretch")
+    for key, (na, ta, no, to) in sorted(acc.items(), key=lambda x: -(x[1][1] + x[1][3]))[:a.top]:
+        ma = ta / na if na else float("nan")
+        mo = to / no if no else float("nan")
+        print(f"{key}, {na}, {ma:.1f}, {no}, {mo:.1f}, {mo / ma if na and no else float('nan'):.2f}")
 
 
 if __name__ == "__main__":
