@@ -89,3 +89,13 @@ def test_trace_summary_steps_and_grid_split(tmp_path):
     assert any(line.startswith("4.00,1,GEMM grid 65536x1x1") for line in lines)
     assert any(line.startswith("2.00,1,GEMM grid 1024x1x1") for line in lines)
     assert any("wgrad16_kernel" in line and "grid 2048" in line for line in lines)
+    # --overlap: the wgrad call (7-9 ms) runs beside the update (7-8 ms) for half its time, so it
+    # counts as alone; --by-predecessor tells the two GEMM grids apart by the kernel before them
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "trace_summary.py"), str(trace), "--steps", "2",
+                          "--overlap", "--by-predecessor"], capture_output=True, text=True, check=True).stdout
+    assert "calls beside the update" in out
+    wl = [line for line in out.splitlines() if line.startswith("pra::wg::wgrad16_kernel")]
+    assert wl and wl[-1].split(", ")[1] == "2" and wl[-1].split(", ")[3] == "0"
+    pred = [line for line in out.splitlines() if line.startswith(("65536, ", "1024, "))]
+    assert any(line.startswith("65536, pra::embed_fwd_kernel<bf16>, 1, 4000.0") for line in pred), pred
+    assert any(line.startswith("1024, GEMM grid 65536, 1, 2000.0") for line in pred), pred
