@@ -120,7 +120,7 @@ at::Tensor rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at::Tens
     dr = dres->data_ptr();
   }
   const int wsr = pra_rmsnorm_bwd_ws_rows((int)rows);
-  at::Tensor ws = at::empty({wsr + 4, D}, h.options().dtype(at::kFloat));
+  at::Tensor ws = at::empty({wsr + pra_rmsnorm_bwd_ws_extra(), D}, h.options().dtype(at::kFloat));
   check(pra_rmsnorm_bwd(dt(h), dy.data_ptr(), h.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(), dr, dx.data_ptr(),
                         dw.data_ptr(), ws.data_ptr<float>(), (int)rows, (int)D, accumulate ? 1 : 0, stream_of(h)),
         "rmsnorm_bwd");
@@ -178,7 +178,7 @@ at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at::Te
   const c10::DeviceGuard guard(h.device());
   at::Tensor dx = at::empty_like(h);
   const int wsr = pra_rmsnorm_bwd_ws_rows((int)rows);
-  at::Tensor ws = at::empty({wsr + 4, 2 * D}, h.options().dtype(at::kFloat));
+  at::Tensor ws = at::empty({wsr + pra_rmsnorm_bwd_ws_extra(), 2 * D}, h.options().dtype(at::kFloat));
   check(pra_layernorm_bwd(dt(h), dy.data_ptr(), h.data_ptr(), w.data_ptr(), mean.data_ptr<float>(),
                           rstd.data_ptr<float>(), dres.has_value() ? dres->data_ptr() : nullptr, dx.data_ptr(),
                           dwb.data_ptr(), ws.data_ptr<float>(), (int)rows, (int)D, accumulate ? 1 : 0, stream_of(h)),

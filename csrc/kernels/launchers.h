@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 extern "C" {
+int pra_rmsnorm_bwd_ws_extra();
 int pra_rmsnorm_bwd_ws_rows(int rows);
 hipError_t pra_rmsnorm_fwd(int dtype, const void* x, const void* delta, const void* w, void* h_out, void* y,
                            float* rstd, int rows, int D, float eps, hipStream_t s);
