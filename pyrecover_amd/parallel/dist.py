@@ -180,10 +180,13 @@ def compare_rccl_order(saved: Optional[dict], current: Optional[dict] = None) ->
 def maybe_init_distributed(activate_distributed: bool, backend: Optional[str] = None,
                            timeout_s: float = 1800.0) -> Tuple[int, int]:
     """Returns (local_rank, world_size). Initializes the process group when a multi-process
-    environment is present (SLURM with >1 tasks, or torchrun with WORLD_SIZE>1)."""
+    environment is present (SLURM with >1 tasks, or torchrun with WORLD_SIZE>1), or when
+    ``--distributed`` is given under torchrun with one process (a 1-rank group)."""
     env = _env_rank_world_local()
     if activate_distributed:
         os.environ["DISTRIBUTED_RUN"] = "1"
+        if env is None and is_torchrun_env():  # torchrun with one process: a 1-rank group, as asked
+            env = (int(os.environ["RANK"]), 1, int(os.environ.get("LOCAL_RANK", 0)))
     if env is None:
         if activate_distributed:
             raise RuntimeError("--distributed was given but no multi-process SLURM/torchrun environment was found")

@@ -250,6 +250,9 @@ def train(args):
         log_rank0(f"Gradient buckets: {reducer.num_buckets}, {sum(reducer.bucket_bytes()) / 2**30:.2f} GiB"
                   f"{(' (RCCL reduce-scatter + all-gather, sharded optimizer)' if shard else ' (RCCL all-reduce)') if is_dist else ''}"
                   f"{', sparse embedding-gradient exchange' if sparse_emb and is_dist else ''}")
+        if reducer.force_collective and not is_dist:
+            log_rank0("Bucket collectives forced on in a 1-rank "
+                      f"{torch.distributed.get_backend()} group (PYRECOVER_FORCE_ALLREDUCE=1)")
     D.set_reducer_settings(bucket_mb=float(bucket_mb) if is_dist else None, allreduce=args.allreduce if is_dist else None,
                            shard_optimizer=shard, sparse_embedding=bool(sparse_emb and is_dist))
     model.train()

@@ -86,6 +86,7 @@ def test_rccl_update_and_checkpoint_streams_together(cuda, tmp_path):
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-4000:]
     assert "backend=nccl" in out, out[-2000:]  # torch's "nccl" backend is RCCL on ROCm
+    assert "Bucket collectives forced on in a 1-rank nccl group" in out, out[-2000:]
     b = tmp_path / "plain"
     env_b = {k: v for k, v in os.environ.items() if k != "PYRECOVER_FORCE_ALLREDUCE"}
     r = subprocess.run([sys.executable, os.path.join(root, "train.py"), "--checkpoint-frequency", "6",
