@@ -59,8 +59,9 @@ def parse():
                     help="record device events around forward / backward / optimizer of each timed step")
     ap.add_argument("--no-comm-timing", action="store_true",
                     help="W > 1: skip the per-bucket collective timing (events; no host sync in the step)")
-    ap.add_argument("--shard-optimizer", action="store_true",
-                    help="W > 1: ZeRO-1 (reduce-scatter, 1/W AdamW update, parameter all-gather; train.py flag)")
+    ap.add_argument("--shard-optimizer", nargs="?", const="on", default="auto", choices=["auto", "on", "off"],
+                    help="W > 1: ZeRO-1 (reduce-scatter, 1/W AdamW update, parameter all-gather; train.py flag); "
+                         "auto: for models without transposed weight shadows at this batch; a bare flag means on")
     ap.add_argument("--sparse-embedding-grad", choices=["auto", "on", "off"], default="auto",
                     help="W > 1: token-embedding gradient as (id, row) pairs (auto: tokens per step <= vocab / 2)")
     ap.add_argument("--comm-probe", choices=["rccl", "all", "off"], default="rccl",
@@ -171,7 +172,10 @@ def main():
         torch.set_default_dtype(torch.bfloat16)
         model = Transformer(cfg)
         torch.set_default_dtype(prev)
-    shard = args.shard_optimizer and world > 1
+    from pyrecover_amd.trainer import _use_shard_optimizer
+
+    shard = _use_shard_optimizer(args.shard_optimizer, world, model, args.batch_per_gpu * args.seq_len,
+                                 dev.type == "cuda")
     flat = model.flatten_(tokens_per_step=args.batch_per_gpu * args.seq_len, shadows=False if shard else None)
     if world > 1:
         broadcast_flat(flat)

@@ -101,9 +101,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--allreduce", choices=["rccl", "xgmi"], default="rccl",
                    help="gradient all-reduce backend: RCCL rings (default) or the direct per-link xGMI "
                         "reduce-scatter/all-gather over IPC-mapped peer buffers (single node)")
-    p.add_argument("--shard-optimizer", action="store_true",
+    p.add_argument("--shard-optimizer", nargs="?", const="on", default="auto", choices=["auto", "on", "off"],
                    help="ZeRO-1 data parallelism: reduce-scatter each gradient bucket, update only this rank's "
-                        "1/W of the parameters, all-gather them (replicated parameters, unchanged checkpoints)")
+                        "1/W of the parameters, all-gather them (replicated parameters, unchanged checkpoints); "
+                        "auto: at W > 1 for 16-bit GPU models that carry no transposed weight shadows at this "
+                        "batch (e.g. Llama-3-8B S2048 B1); a bare flag means on")
     p.add_argument("--sparse-embedding-grad", choices=["auto", "on", "off"], default="auto",
                    help="reduce the token-embedding gradient as (token id, row) pairs instead of a dense "
                         "all-reduce; auto: when the ranks' tokens per step are at most half the vocabulary")

@@ -217,17 +217,22 @@ class Transformer(nn.Module):
             self.flat = FlatParams(self.fusion_groups())
             # optimizer-state indices follow model.parameters() order, as in the reference
             self.flat.module_order = list(self.parameters())
-            if shadows is None:
-                shadows = os.environ.get("PRA_WEIGHT_SHADOWS", "auto")
-            if str(shadows).strip().lower() == "auto":
-                gqa = self.model_args.kv_heads < self.model_args.n_heads
-                shadows = not (gqa and tokens_per_step is not None and tokens_per_step <= 4096)
-            self.flat.shadow_sites = self.shadow_sites(shadows)
+            self.flat.shadow_sites = self.planned_shadow_sites(tokens_per_step, shadows)
             for mats in self._gemm_weights(self.flat.shadow_sites):
                 self.flat.register_transposed(mats, (sum(p.shape[0] for p in mats), mats[0].shape[1]))
             # parameters written through the module API must refresh the transposed shadows
             self.register_load_state_dict_post_hook(lambda mod, keys: mod.flat.refresh_transposed())
         return self.flat
+
+    def planned_shadow_sites(self, tokens_per_step: Optional[int] = None, shadows=None) -> Tuple[str, ...]:
+        """The sites flatten_ gives a shadow (before any buffer exists; the shadows themselves are only
+        registered for 16-bit GPU buffers)."""
+        if shadows is None:
+            shadows = os.environ.get("PRA_WEIGHT_SHADOWS", "auto")
+        if str(shadows).strip().lower() == "auto":
+            gqa = self.model_args.kv_heads < self.model_args.n_heads
+            shadows = not (gqa and tokens_per_step is not None and tokens_per_step <= 4096)
+        return self.shadow_sites(shadows)
 
     @classmethod
     def shadow_sites(cls, spec) -> Tuple[str, ...]:

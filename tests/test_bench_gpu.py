@@ -63,6 +63,20 @@ def test_bench_gpus2_sharded_optimizer_sparse_embedding_replicas_identical(cuda)
     assert abs(zero["final_loss"] - dense["final_loss"]) < 0.05 * abs(dense["final_loss"]) + 1e-3
 
 
+def test_bench_gpus2_auto_shards_a_gqa_batch1_job(cuda):
+    """--shard-optimizer auto (the default): a grouped-query model at batch 1 carries no weight
+    shadows, so a 2-rank job runs ZeRO-1 on its own, and its replicas end bitwise identical."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(PYRECOVER_LOCAL_DEVICE="0", PYRECOVER_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--model", "llama-tiny",
+                        "--batch-per-gpu", "1", "--seq-len", "256", "--steps", "3", "--warmup", "1",
+                        "--bucket-mb", "0.25"], capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-5000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')][-1])
+    assert out["config"]["shard_optimizer"] is True and not out["config"]["weight_shadows"]
+    assert out["params_identical_across_ranks"] is True
+
+
 def test_replica_checksum_kernel_matches_torch(cuda):
     """pra_checksum (csrc/kernels/comm.hip) against the torch definition: the 64-bit word hash is
     exact, the fp64 element sum equal to rounding; one flipped bit changes the hash."""

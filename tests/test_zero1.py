@@ -306,3 +306,22 @@ def test_checkpoint_bytes_counts_the_fp32_master(tmp_path):
         save_ckpt_vanilla(m, opt, None, None, 1, 1, str(p), max_keep=0, verify=False)
         size = p.stat().st_size
         assert per * nparam <= size <= per * nparam * 1.02 + (2 << 20), (mw, size, per * nparam)
+
+
+def test_shard_optimizer_auto_policy():
+    """--shard-optimizer auto: ZeRO-1 at W > 1 for a 16-bit GPU model that carries no transposed
+    weight shadows at its batch (grouped-query attention at <= 4096 tokens per rank); never at
+    W = 1, for CPU / fp32 models, or when the model keeps shadows; on / off / a bare flag override."""
+    from pyrecover_amd.config import get_preset
+    from pyrecover_amd.models.llama import Transformer
+    from pyrecover_amd.trainer import _use_shard_optimizer
+
+    gqa = Transformer(get_preset("llama-micro", seq_len=64))  # 2 heads, 1 kv head
+    mha = Transformer(get_preset("llama-micro", seq_len=64, n_kv_heads=2))
+    assert _use_shard_optimizer("auto", 8, gqa, 2048, True)
+    assert not _use_shard_optimizer("auto", 8, gqa, 8192, True)  # shadows pay at 8192 tokens
+    assert not _use_shard_optimizer("auto", 8, mha, 2048, True)
+    assert not _use_shard_optimizer("auto", 1, gqa, 2048, True)
+    assert not _use_shard_optimizer("auto", 8, gqa, 2048, False)  # CPU or fp32
+    assert _use_shard_optimizer("on", 2, mha, 32768, False) and _use_shard_optimizer(True, 2, mha, 32768, True)
+    assert not _use_shard_optimizer("off", 8, gqa, 2048, True)

@@ -21,6 +21,12 @@ in-order side stream, optim/adamw.py), for each DP mode:
 exposed = max(last comm end, last update end) - bwd_end, minus the same quantity on one GPU (where
 the updates already run beside the backward inside the measured step), so
     predicted step (N) = 1-GPU step + exposed(N) - exposed(1).
+In the shard mode each rank updates 1/N of every bucket, so the update's cost INSIDE the step
+(measured: the 1-GPU step with and without the update kernels, ``update_in_step_ms``) shrinks
+with it, assumed in proportion to the bytes:
+    predicted step (N, shard) = 1-GPU step - update_in_step (1 - 1/N) + exposed(N) - exposed(1).
+A model with transposed weight shadows loses them in the shard mode (models/llama.py); that
+difference is not modelled, and the row says so.
 ``adamw_ms`` is the whole-model update timed alone on this GPU. Not modelled: the CUs RCCL's
 kernels take from compute while they overlap it.
 
@@ -151,6 +157,26 @@ def main():
         if not timed:
             timer.steps.clear()
     torch.cuda.synchronize()
+    # the same step without the update kernels: what the update costs inside the step
+    real_update = opt._update_range
+    opt._update_range = lambda *args, **kw: None
+    reducer.timer = None  # the recorded steps above stay as they are
+    nou = []
+    for i in range(a.warmup + a.steps):
+        t = torch.randint(0, cfg.vocab_size, (B, S + 1), device=dev, generator=gen)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        opt.zero_grad()
+        model(t[:, :-1], labels=t[:, 1:]).backward()
+        reducer.finish()
+        opt.step()
+        e1.record()
+        if i >= a.warmup:
+            nou.append((e0, e1))
+    torch.cuda.synchronize()
+    opt._update_range = real_update
+    reducer.timer = timer
+    noupdate_ms = sum(x.elapsed_time(y) for x, y in nou) / len(nou)
     # the whole-model AdamW update alone on this GPU (the per-bucket updates of the model)
     upd_ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     for rep in range(3):
@@ -201,7 +227,11 @@ def main():
             exp, ends, uends = simulate(ready, bwd_end, nbytes, a.world, bw, a.latency_us, adamw_ms, mode,
                                         sparse_bytes if sp else None, sparse_extra if sp else 0.0)
             pred = span + exp - exp1
-            rows.append({"mode": mode + ("+sparse" if sp else ""), "busbw_gbps": bw,
+            if mode == "shard":
+                pred -= max(0.0, span - noupdate_ms) * (1.0 - 1.0 / a.world)
+            shadows = bool(getattr(flat, "shadow_sites", ())) and mode == "shard"
+            rows.append({"mode": mode + ("+sparse" if sp else "") + (" (shadows lost: not modelled)" if shadows else ""),
+                         "busbw_gbps": bw,
                          "comm_end_ms": round(max(ends), 2), "update_end_ms": round(max(uends), 2),
                          "exposed_ms": round(exp, 2), "predicted_step_ms": round(pred, 1),
                          "predicted_scaling_eff": round(span / pred, 4)})
@@ -209,12 +239,13 @@ def main():
            "buckets": nb, "grad_gib": round(sum(nbytes) / 2**30, 3), "step_ms_1gpu": round(span, 1),
            "bwd_end_ms": round(bwd_end, 1), "first_ready_ms": round(ready[0], 1), "last_ready_ms": round(ready[-1], 1),
            "adamw_alone_ms": round(adamw_ms, 2), "exposed_1gpu_ms": round(exp1, 2),
+           "step_ms_1gpu_without_update": round(noupdate_ms, 1), "update_in_step_ms": round(span - noupdate_ms, 1),
            "sparse_exchange_mib": round(sparse_bytes / 2**20, 1) if sparse_bytes else None,
            "sparse_local_ms": round(sparse_extra, 2), "latency_us": a.latency_us, "rows": rows,
            "ready_ms": [round(x, 2) for x in ready], "bucket_mib": [round(x / 2**20, 1) for x in nbytes]}
     print(f"{a.model} B{B} S{S}: 1-GPU step {span:.1f} ms, backward ends at {bwd_end:.1f} ms; {nb} buckets "
           f"({out['grad_gib']} GiB), ready {ready[0]:.1f} .. {ready[-1]:.1f} ms; AdamW alone {adamw_ms:.1f} ms "
-          f"(1-GPU update tail {exp1:.2f} ms)")
+          f"(1-GPU update tail {exp1:.2f} ms; the step without the update {noupdate_ms:.1f} ms)")
     print(f"| mode | busbw GB/s | comm ends ms | updates end ms | exposed ms | predicted step ms (N={a.world}) | "
           f"scaling eff |")
     print("|---|---|---|---|---|---|---|")
