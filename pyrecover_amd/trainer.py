@@ -697,7 +697,7 @@ def _use_shard_optimizer(mode, world: int, model, tokens_per_rank: int, gpu16: b
     gets no transposed weight shadows at this batch (models/llama.py planned_shadow_sites; the
     sharded mode runs without them). Then ZeRO-1 costs the step nothing and each rank updates 1/W
     of the parameters: Llama-3-8B S2048 B1 at N = 8 predicted 0.85 -> 0.89 scaling at 300 GB/s
-    with the sparse embedding exchange (profiles/r6/comm/comm_predict_8b_b1.log). A bare
+    with the sparse embedding exchange (profiles/r6/comm/comm_predict_8b_b1_with_update_cost.log). A bare
     ``--shard-optimizer`` (True) means on."""
     if world <= 1 or mode in (False, None, "off"):
         return False
