@@ -276,6 +276,8 @@ def train(args):
         from .graph import capture_allowed
 
         cap_ok, cap_why = capture_allowed(world_size)
+        if cap_ok and (shard or (sparse_emb and is_dist)):  # host-side bookkeeping between collectives
+            cap_ok, cap_why = False, "the sharded optimizer / sparse embedding exchange are not captured"
         if not cap_ok:
             log_rank0(f"--compile: running eagerly: {cap_why}")
         elif use_cuda:
