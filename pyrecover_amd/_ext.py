@@ -88,6 +88,12 @@ def _attn_env() -> dict:
                 env[key] = int(v)
             except ValueError:
                 raise ValueError(f"{name}={v!r} is not a valid int") from None
+    # PYRECOVER_ATTN_BWD_FUSED=1 selects the fused backward by shape: only where its grid (one
+    # workgroup per batch x kv head) fills the chip. At batch 1 (8 workgroups for Llama-3-8B) it was
+    # 78% slower, so it never runs there (round-5 verdict). set_attn_options(bwd_fused=1) still
+    # forces it at every shape (kernel tests).
+    if env.get("bwd_fused") == 1:
+        env["bwd_fused"] = -1
     return env
 
 

@@ -137,3 +137,14 @@ def test_weight_shadow_site_policy(monkeypatch):
     monkeypatch.setenv("PRA_WEIGHT_SHADOWS", "w13,head")
     flat = Transformer(get_preset("llama-tiny", seq_len=64, n_kv_heads=2)).flatten_(tokens_per_step=2048)
     assert flat.shadow_sites == ("w13", "head")  # (shadows themselves exist only for 16-bit GPU buffers)
+
+
+def test_fused_attention_backward_env_selects_by_shape(monkeypatch):
+    """PYRECOVER_ATTN_BWD_FUSED=1 means the fused backward where its grid fills the chip (launcher
+    mode -1), so a batch-1 job never runs it; 0 keeps the split kernels."""
+    from pyrecover_amd import _ext
+
+    monkeypatch.setenv("PYRECOVER_ATTN_BWD_FUSED", "1")
+    assert _ext._attn_env() == {"bwd_fused": -1}
+    monkeypatch.setenv("PYRECOVER_ATTN_BWD_FUSED", "0")
+    assert _ext._attn_env() == {"bwd_fused": 0}
